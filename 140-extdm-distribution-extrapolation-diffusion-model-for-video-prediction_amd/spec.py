@@ -1,0 +1,187 @@
+"""Model configuration and state_dict layout of the ExtDM sampling path.
+
+`unet_spec(cfg)` lists the Unet3D state_dict entries (name, shape, dtype) in the
+exact order the reference registers them
+(model/BaseDM_adaptor/DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12.py:864-1003),
+so reference DM checkpoints (`checkpoint['diffusion']`, keys `denoise_fn.*`)
+load strict-compatible and synthetic weights are generated in reference order.
+`generator_spec(gcfg)` does the same for the LFAE Generator decoder
+(model/LFAE/generator.py:26-62, util.py:69-149).
+"""
+import math
+from dataclasses import dataclass, field
+
+ARCH_U12 = 'DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12'
+ARCH_U22 = 'DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u22'  # byte-identical to u12
+ARCH_IDS = {ARCH_U12: 0, ARCH_U22: 0}
+
+
+@dataclass
+class UnetConfig:
+    """Constructor surface of Unet3D as FlowDiffusion builds it
+    (VideoFlowDiffusion_multi_w_ref.py:80-94)."""
+    dim: int = 64
+    channels: int = 512
+    dim_mults: tuple = (1, 2, 4, 4)
+    window: tuple = (2, 4, 4)
+    heads: int = 8
+    dim_head: int = 32
+    tc: int = 2
+    tp: int = 14
+    latent: int = 32           # flow / latent H = W
+    fea_size: int = 16         # cond_fea spatial size (LFAE bottleneck)
+    fea_ch: int = 256
+    arch: str = ARCH_U12
+
+    def levels(self):
+        dims = [self.dim] + [self.dim * m for m in self.dim_mults]
+        return list(zip(dims[:-1], dims[1:]))
+
+    def as_dict(self):
+        return {'dim': self.dim, 'dim_mults': tuple(self.dim_mults), 'window': tuple(self.window),
+                'heads': self.heads, 'dim_head': self.dim_head, 'tc': self.tc, 'tp': self.tp}
+
+
+def adaptor_layers(tm, tp):
+    """compute_layer (u12:644-648)."""
+    L = max(1, int(math.ceil(math.log2((tp + 1) / tm))))
+    return L, (2 ** L - 1) * tm
+
+
+def _resnet(out, p, din, dout, temb_dim):
+    if temb_dim:
+        out += [(f'{p}.mlp.1.weight', (dout * 2, temb_dim)), (f'{p}.mlp.1.bias', (dout * 2,))]
+    for b, ci in (('block1', din), ('block2', dout)):
+        out += [(f'{p}.{b}.proj.weight', (dout, ci, 1, 3, 3)), (f'{p}.{b}.proj.bias', (dout,)),
+                (f'{p}.{b}.norm.weight', (dout,)), (f'{p}.{b}.norm.bias', (dout,))]
+    if din != dout:
+        out += [(f'{p}.res_conv.weight', (dout, din, 1, 1, 1)), (f'{p}.res_conv.bias', (dout,))]
+
+
+def _stw(out, p, d, cfg):
+    a = f'{p}.fn.fn.attn'
+    w = cfg.window
+    nt = (2 * w[0] - 1) * (2 * w[1] - 1) * (2 * w[2] - 1)
+    N = w[0] * w[1] * w[2]
+    hid = cfg.heads * cfg.dim_head
+    out += [(f'{a}.relative_position_bias_table', (nt, cfg.heads)),
+            (f'{a}.relative_position_index', (N, N), 'int64'),
+            (f'{a}.rotary_emb.freqs', (min(32, cfg.dim_head) // 2,)),
+            (f'{a}.qkv.weight', (3 * hid, d)),
+            (f'{a}.proj.weight', (d, hid)), (f'{a}.proj.bias', (d,)),
+            (f'{p}.fn.norm.gamma', (1, d, 1, 1, 1))]
+
+
+def _adaptor(out, p, d, cfg):
+    L, Fr = adaptor_layers(cfg.tc, cfg.tp)
+    ap = f'{p}.adaptors'
+    out += [(f'{ap}.predictor.fn.fn.weight', (d, d, 1, 1, 1)), (f'{ap}.predictor.fn.fn.bias', (d,)),
+            (f'{ap}.predictor.fn.norm.gamma', (1, d, 1, 1, 1))]
+    for l in range(L):
+        out += [(f'{ap}.extrapolators.{l}.fn.weight', (d, d, 1, 3, 3))]
+    out += [(f'{p}.Tmodulator.weight', (d * cfg.tp, d * Fr, 1, 1)), (f'{p}.Tmodulator.bias', (d * cfg.tp,)),
+            (f'{p}.fuser.fn.weight', (d, 2 * d, 1, 1, 1)), (f'{p}.fuser.fn.bias', (d,)),
+            (f'{p}.fuser.norm.gamma', (1, 2 * d, 1, 1, 1))]
+
+
+def unet_spec(cfg: UnetConfig):
+    """Ordered (name, shape, dtype) list of the u12 Unet3D state_dict."""
+    out = []
+    hid = cfg.heads * cfg.dim_head
+    d0 = cfg.dim
+    tdim = cfg.dim * 4
+    out += [('time_rel_pos_bias.relative_attention_bias.weight', (32, cfg.heads)),
+            ('init_conv.weight', (d0, cfg.channels, 1, 7, 7)), ('init_conv.bias', (d0,)),
+            ('init_noise_conv.weight', (256, 3, 1, 7, 7)), ('init_noise_conv.bias', (256,))]
+    a = 'init_temporal_attn.fn.fn.fn'
+    out += [(f'{a}.norm.weight', (d0,)), (f'{a}.norm.bias', (d0,)),
+            (f'{a}.attn.rotary_emb.freqs', (min(32, cfg.dim_head) // 2,)),
+            (f'{a}.attn.to_qkv.weight', (3 * hid, d0)), (f'{a}.attn.to_out.weight', (d0, hid)),
+            ('init_temporal_attn.fn.norm.gamma', (1, d0, 1, 1, 1))]
+    _adaptor(out, 'init_adaptor', 256, cfg)
+    for n in ('q', 'k', 'v', 'o'):
+        out += [(f'init_traj.cross_att.linear_{n}.weight', (256, 256)),
+                (f'init_traj.cross_att.linear_{n}.bias', (256,))]
+    out += [('init_traj.fuser.weight', (256, 512, 1, 1, 1)), ('init_traj.fuser.bias', (256,)),
+            ('time_mlp.1.weight', (tdim, cfg.dim)), ('time_mlp.1.bias', (tdim,)),
+            ('time_mlp.3.weight', (tdim, tdim)), ('time_mlp.3.bias', (tdim,))]
+    lv = cfg.levels()
+    for i, (din, dout) in enumerate(lv):
+        p = f'downs.{i}'
+        _resnet(out, p + '.0', din, dout, tdim)
+        _stw(out, p + '.1', dout, cfg)
+        _resnet(out, p + '.2', dout, dout, tdim)
+        _stw(out, p + '.3', dout, cfg)
+        if i > 1:
+            _adaptor(out, p + '.4', dout, cfg)
+        if i < len(lv) - 1:
+            out += [(f'{p}.5.weight', (dout, dout, 1, 4, 4)), (f'{p}.5.bias', (dout,))]
+    for i, (din, dout) in enumerate(reversed(lv)):
+        p = f'ups.{i}'
+        _resnet(out, p + '.0', dout * 2, din, tdim)
+        _stw(out, p + '.1', din, cfg)
+        _resnet(out, p + '.2', din, din, tdim)
+        _stw(out, p + '.3', din, cfg)
+        if i > 1:
+            _adaptor(out, p + '.4', din, cfg)
+        if i < len(lv) - 1:
+            out += [(f'{p}.5.weight', (din, din, 1, 4, 4)), (f'{p}.5.bias', (din,))]
+    # the `ups` ModuleList is registered before mid_block1 (u12:946-947)
+    md = lv[-1][1]
+    _resnet(out, 'mid_block1', md, md, tdim)
+    _stw(out, 'mid_attn1', md, cfg)
+    _resnet(out, 'mid_block2', md, md, tdim)
+    _stw(out, 'mid_attn2', md, cfg)
+    _adaptor(out, 'mid_adaptor', md, cfg)
+    for head, oc in (('final_conv', 2), ('occlusion_map', 1)):
+        _resnet(out, head + '.0', cfg.dim * 2, cfg.dim, 0)
+        out += [(f'{head}.1.weight', (oc, cfg.dim, 1, 1, 1)), (f'{head}.1.bias', (oc,))]
+    return [(e[0], tuple(e[1]), e[2] if len(e) > 2 else 'float32') for e in out]
+
+
+@dataclass
+class GeneratorConfig:
+    """LFAE Generator decoder surface (config/DM/*.yaml flow_params.generator_params)."""
+    num_channels: int = 3
+    block_expansion: int = 64
+    max_features: int = 512
+    num_down_blocks: int = 2
+    num_bottleneck_blocks: int = 6
+    image: int = 64
+
+    def as_dict(self):
+        return {'num_down_blocks': self.num_down_blocks, 'num_bottleneck_blocks': self.num_bottleneck_blocks}
+
+
+def _bn(out, p, c):
+    out += [(f'{p}.weight', (c,)), (f'{p}.bias', (c,)), (f'{p}.running_mean', (c,)),
+            (f'{p}.running_var', (c,)), (f'{p}.num_batches_tracked', (), 'int64')]
+
+
+def generator_spec(g: GeneratorConfig, prefix=''):
+    """Decoder-side Generator entries (first, down_blocks, up_blocks, bottleneck,
+    final) in reference registration order (generator.py:26-62). The
+    pixelwise_flow_predictor (encoder side) is registered first in
+    the reference and is not listed here."""
+    out = []
+    be, mf = g.block_expansion, g.max_features
+    out += [(f'{prefix}first.conv.weight', (be, g.num_channels, 7, 7)), (f'{prefix}first.conv.bias', (be,))]
+    _bn(out, f'{prefix}first.norm', be)
+    for i in range(g.num_down_blocks):
+        ci, co = min(mf, be * 2 ** i), min(mf, be * 2 ** (i + 1))
+        out += [(f'{prefix}down_blocks.{i}.conv.weight', (co, ci, 3, 3)), (f'{prefix}down_blocks.{i}.conv.bias', (co,))]
+        _bn(out, f'{prefix}down_blocks.{i}.norm', co)
+    for i in range(g.num_down_blocks):
+        ci = min(mf, be * 2 ** (g.num_down_blocks - i))
+        co = min(mf, be * 2 ** (g.num_down_blocks - i - 1))
+        out += [(f'{prefix}up_blocks.{i}.conv.weight', (co, ci, 3, 3)), (f'{prefix}up_blocks.{i}.conv.bias', (co,))]
+        _bn(out, f'{prefix}up_blocks.{i}.norm', co)
+    c = min(mf, be * 2 ** g.num_down_blocks)
+    for i in range(g.num_bottleneck_blocks):
+        p = f'{prefix}bottleneck.r{i}'
+        out += [(f'{p}.conv1.weight', (c, c, 3, 3)), (f'{p}.conv1.bias', (c,)),
+                (f'{p}.conv2.weight', (c, c, 3, 3)), (f'{p}.conv2.bias', (c,))]
+        _bn(out, f'{p}.norm1', c)
+        _bn(out, f'{p}.norm2', c)
+    out += [(f'{prefix}final.weight', (g.num_channels, be, 7, 7)), (f'{prefix}final.bias', (g.num_channels,))]
+    return [(e[0], tuple(e[1]), e[2] if len(e) > 2 else 'float32') for e in out]

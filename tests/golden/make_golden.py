@@ -1,0 +1,165 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE
+itself (read-only at /root/reference) on CPU in the build container.
+
+Only data leaves this script: inputs are regenerated from seeds at test time,
+outputs/checksums are stored as .npz/.json. Missing third-party packages are
+replaced by the stand-ins under tests/golden/shims/ (einops_exts, timm,
+skimage: import-only; rotary_embedding_torch: restatement of 0.8.3).
+
+Usage (build container only):  python tests/golden/make_golden.py
+"""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = '/root/reference'
+
+sys.path.insert(0, REPO)
+from tests.golden_inputs import CONFIGS, GEN_CFG, unet_inputs, decoder_inputs, make_sd, make_gen_sd, PKG  # noqa: E402
+
+spec = importlib.import_module(PKG + '.spec')
+
+
+def import_reference():
+    sys.path.insert(0, os.path.join(HERE, 'shims'))
+    sys.path.insert(0, REF)
+    torch.nn.Module.cuda = lambda self, *a, **k: self
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    from model.BaseDM_adaptor.DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12 import Unet3D
+    from model.BaseDM_adaptor.Diffusion import GaussianDiffusion
+    from model.LFAE.generator import Generator
+    return Unet3D, GaussianDiffusion, Generator
+
+
+def build_ref_unet(Unet3D, cfg):
+    return Unet3D(dim=cfg.dim, channels=cfg.channels, out_grid_dim=2, out_conf_dim=1, dim_mults=cfg.dim_mults,
+                  use_bert_text_cond=False, learn_null_cond=False, use_final_activation=False, use_deconv=True,
+                  padding_mode='zeros', cond_num=cfg.tc, pred_num=cfg.tp, framesize=cfg.latent).eval()
+
+
+def main():
+    torch.set_num_threads(8)
+    Unet3D, GaussianDiffusion, Generator = import_reference()
+    keys = {}
+    for name, cfg in CONFIGS.items():
+        net = build_ref_unet(Unet3D, cfg)
+        ref_sd = net.state_dict()
+        keys[name] = [[k, list(v.shape), str(v.dtype).replace('torch.', '')] for k, v in ref_sd.items()]
+        sd = make_sd(cfg)
+        net.load_state_dict(sd, strict=True)
+        # hooks on a few intermediate modules (per-module goldens)
+        taps = {}
+        watch = ['init_traj', 'init_temporal_attn', 'downs.0.0', 'downs.0.1', 'downs.1.3', 'downs.2.4',
+                 'mid_attn1', 'mid_adaptor', 'ups.0.5', 'ups.3.4', 'final_conv']
+        mods = dict(net.named_modules())
+        for w in watch:
+            mods[w].register_forward_hook(lambda m, i, o, w=w: taps.__setitem__(w, o.detach().clone()))
+        x, t, cond, fea = unet_inputs(cfg)
+        with torch.no_grad():
+            eps = net(x, t, cond, cond_fea=fea)
+        out = {'eps': eps.numpy()}
+        for w, v in taps.items():
+            if name == 'small':
+                out['tap_' + w] = v.numpy()
+            out['tapsum_' + w] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+        np.savez_compressed(os.path.join(HERE, f'unet_{name}.npz'), **out)
+        print(name, 'eps', eps.shape, float(eps.abs().mean()))
+
+        if name == 'small':
+            # samplers with the small net
+            dd = GaussianDiffusion(net, image_size=cfg.latent, num_frames=cfg.tc + cfg.tp, timesteps=1000,
+                                   sampling_timesteps=1000, loss_type='l2', use_dynamic_thres=True,
+                                   null_cond_prob=0.0)
+            sch = {k: v.numpy() for k, v in dd.named_buffers()}
+            np.savez_compressed(os.path.join(HERE, 'schedule_1000.npz'), **sch)
+            steps = {}
+            with torch.no_grad():
+                for ti in (999, 500, 1, 0):
+                    tt = torch.full((x.shape[0],), ti, dtype=torch.long)
+                    mean, _, logv = dd.p_mean_variance(cond, x, fea, tt, clip_denoised=True, cond_scale=1.)
+                    torch.manual_seed(100 + ti)
+                    steps[f'p_sample_{ti}'] = dd.p_sample(cond, x, fea, tt).numpy()
+                    steps[f'mean_{ti}'] = mean.numpy()
+                    steps[f'logvar_{ti}'] = logv.reshape(-1).numpy()
+                # short DDPM chain: timesteps=10 => p_sample_loop runs 10 steps
+                d10 = GaussianDiffusion(net, image_size=cfg.latent, num_frames=cfg.tc + cfg.tp, timesteps=10,
+                                        sampling_timesteps=10, null_cond_prob=0.0)
+                # The reference's p_sample_loop cannot run as written: Diffusion.py:186 passes t
+                # positionally into p_sample's `cond_fea` slot and cond_fea again by keyword
+                # (TypeError). Record that, then drive the reference's own p_sample with the
+                # evident binding p_sample(x_cond, img, cond_fea, t) in the loop's RNG order.
+                try:
+                    d10.sample(cond, cond_fea=fea)
+                    steps['p_sample_loop_raises'] = np.array(0)
+                except TypeError:
+                    steps['p_sample_loop_raises'] = np.array(1)
+                torch.manual_seed(7)
+                img = torch.randn(x.shape)
+                for i in reversed(range(10)):
+                    img = d10.p_sample(cond, img, fea, torch.full((x.shape[0],), i, dtype=torch.long))
+                steps['ddpm10'] = img.numpy()
+                # DDIM-10 over the 1000-step schedule
+                dI = GaussianDiffusion(net, image_size=cfg.latent, num_frames=cfg.tc + cfg.tp, timesteps=1000,
+                                       sampling_timesteps=10, ddim_sampling_eta=1.0, null_cond_prob=0.0)
+                torch.manual_seed(11)
+                steps['ddim10'] = dI.sample(cond, cond_fea=fea).numpy()
+            np.savez_compressed(os.path.join(HERE, 'sampler_small.npz'), **steps)
+
+    with open(os.path.join(HERE, 'unet_keys.json'), 'w') as f:
+        json.dump(keys, f)
+
+    # DDIM pair lists (Diffusion.py:214-216)
+    pairs = {}
+    for S in (10, 100, 250):
+        times = torch.linspace(0., 1000, steps=S + 2)[:-1]
+        times = list(reversed(times.int().tolist()))
+        pairs[str(S)] = list(zip(times[:-1], times[1:]))
+    with open(os.path.join(HERE, 'ddim_pairs.json'), 'w') as f:
+        json.dump(pairs, f)
+
+    # torch.quantile on crafted ties / boundaries (the reference's threshold op)
+    qs = {}
+    g = torch.Generator().manual_seed(3)
+    cases = {
+        'ties': torch.tensor([[1., 1., 1., 2., 2., 2., 3., 3., 3., 3.]]),
+        'random': torch.randn(3, 43008, generator=g).abs(),
+        'spike': torch.cat([torch.zeros(1, 40000), torch.full((1, 3008), 5.0)], dim=1),
+        'tiny': torch.rand(2, 7, generator=g),
+        'lowval': torch.rand(2, 1000, generator=g) * 1e-3,
+    }
+    for k, v in cases.items():
+        qs[k + '_in'] = v.numpy()
+        qs[k + '_out'] = torch.quantile(v, 0.9, dim=-1).numpy()
+    np.savez_compressed(os.path.join(HERE, 'quantile.npz'), **qs)
+
+    # LFAE decoder (Generator.forward_with_flow), with and without occlusion
+    gen = Generator(num_regions=10, num_channels=3, revert_axis_swap=True,
+                    block_expansion=GEN_CFG.block_expansion, max_features=GEN_CFG.max_features,
+                    num_down_blocks=GEN_CFG.num_down_blocks, num_bottleneck_blocks=GEN_CFG.num_bottleneck_blocks,
+                    skips=True, pixelwise_flow_predictor_params=dict(
+                        block_expansion=64, max_features=1024, num_blocks=5, scale_factor=0.5,
+                        use_deformed_source=True, use_covar_heatmap=True, estimate_occlusion_map=True)).eval()
+    gsd = make_gen_sd()
+    missing, unexpected = gen.load_state_dict(gsd, strict=False)
+    assert not unexpected, unexpected
+    assert all(m.startswith('pixelwise_flow_predictor') for m in missing), missing
+    gkeys = [[k, list(v.shape)] for k, v in gen.state_dict().items() if not k.startswith('pixelwise_flow_predictor')]
+    with open(os.path.join(HERE, 'generator_keys.json'), 'w') as f:
+        json.dump(gkeys, f)
+    src, flow, occ = decoder_inputs()
+    with torch.no_grad():
+        r1 = gen.forward_with_flow(src, flow, occ)
+        r0 = gen.forward_with_flow(src, flow, None)
+    np.savez_compressed(os.path.join(HERE, 'decoder.npz'), pred_occ=r1['prediction'].numpy(),
+                        deformed=r1['deformed'].numpy(), pred_noocc=r0['prediction'].numpy())
+    print('done')
+
+
+if __name__ == '__main__':
+    main()
