@@ -1,0 +1,7 @@
+"""MI355X-native ExtDM sampling path (gfx950 HIP kernels behind a C ABI).
+
+Import with importlib (the directory name is not a Python identifier):
+    pkg = importlib.import_module('140-extdm-distribution-extrapolation-diffusion-model-for-video-prediction_amd')
+"""
+from . import spec, weights, _lib  # noqa: F401
+from .models import Unet3D, GaussianDiffusion, Generator, schedule_buffers, ddim_time_pairs  # noqa: F401

@@ -1,0 +1,48 @@
+"""Build libextdm_hip.so (gfx950) in-tree with hipcc: the .so travels with the
+repository snapshot to the GPU box. No torch extension machinery is involved."""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, 'csrc')
+REPO = os.path.dirname(HERE)
+INCLUDE = os.path.join(REPO, 'include')
+LIB = os.path.join(HERE, 'libextdm_hip.so')
+SOURCES = ['conv.hip', 'norm.hip', 'attn.hip', 'sampler.hip', 'runtime.cpp']
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-I', INCLUDE, '-I', CSRC]
+
+
+def _needs(obj, src):
+    if not os.path.exists(obj):
+        return True
+    deps = [src, os.path.join(CSRC, 'kernels.h'), os.path.join(INCLUDE, 'extdm.h')]
+    return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
+
+
+def _compile(src):
+    obj = os.path.join(CSRC, 'build', src + '.o')
+    s = os.path.join(CSRC, src)
+    if _needs(obj, s):
+        cmd = [HIPCC] + FLAGS + (['-x', 'hip'] if src.endswith('.cpp') else []) + ['-c', s, '-o', obj]
+        subprocess.run(cmd, check=True)
+    return obj
+
+
+def build(verbose=False):
+    os.makedirs(os.path.join(CSRC, 'build'), exist_ok=True)
+    jobs = int(os.environ.get('MAX_JOBS', '8'))
+    with ThreadPoolExecutor(max_workers=min(jobs, len(SOURCES))) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    if not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
+        subprocess.run([HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', LIB] + objs, check=True)
+    if verbose:
+        print('built', LIB)
+    return LIB
+
+
+if __name__ == '__main__':
+    build(verbose=True)
+    sys.exit(0)

@@ -1,0 +1,121 @@
+// ExtDM sampling path — HIP kernels for gfx950 (MI355X / CDNA4).
+//
+// Layout convention: every activation is a 5-D view [B][C][T][H][W] with
+// contiguous H*W planes and explicit batch/channel/frame strides (elements).
+// Channel-first buffers (sc = T*H*W, st = H*W) are the reference's NCDHW; the
+// MotionAdaptor's work buffers are frame-major (sc = H*W, st = C*H*W) so that
+// its '(T C)' channel flattening (u12:709) is a plain stride.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace extdm {
+
+struct View {
+  float* p = nullptr;
+  int B = 0, C = 0, T = 0, H = 0, W = 0;
+  long sb = 0, sc = 0, st = 0;  // strides in elements; plane stride = W, pixel stride = 1
+  int HW() const { return H * W; }
+  long numel() const { return (long)B * C * T * H * W; }
+  View frames(int t0, int n) const {
+    View v = *this; v.p = p + (long)t0 * st; v.T = n; return v;
+  }
+  View chans(int c0, int n) const {
+    View v = *this; v.p = p + (long)c0 * sc; v.C = n; return v;
+  }
+};
+
+inline View cf_view(float* p, int B, int C, int T, int H, int W) {  // channel-first
+  View v; v.p = p; v.B = B; v.C = C; v.T = T; v.H = H; v.W = W;
+  v.st = (long)H * W; v.sc = (long)T * H * W; v.sb = (long)C * T * H * W; return v;
+}
+inline View tm_view(float* p, int B, int C, int T, int H, int W) {  // frame-major
+  View v; v.p = p; v.B = B; v.C = C; v.T = T; v.H = H; v.W = W;
+  v.sc = (long)H * W; v.st = (long)C * H * W; v.sb = (long)C * T * H * W; return v;
+}
+
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_SILU = 3, ACT_SIGMOID = 4 };
+enum ConvMode { MODE_CONV = 0, MODE_DECONV = 1, MODE_UP2 = 2 };
+
+// Packed GEMM weight: A[k][m] (k = ci*KH*KW + ky*KW + kx), zero padded to
+// Kpad x Mpad; for MODE_DECONV four parity planes back to back.
+struct PackedW {
+  float* w = nullptr;
+  int K = 0, M = 0, Kpad = 0, Mpad = 0, KH = 1, KW = 1, mode = MODE_CONV;
+};
+
+// Output-channel tile of the conv GEMM for M output channels (Mpad is a multiple of it).
+inline int conv_bm(int M) { return M <= 32 ? 32 : ((M <= 64 || M % 128 != 0) ? 64 : 128); }
+
+struct ConvEpi {
+  const float* bias = nullptr;     // [Cout]
+  const float* res = nullptr;      // residual view (same B,T,H,W as out)
+  long res_sb = 0, res_sc = 0, res_st = 0;
+  const float* post_scale = nullptr;  // [B][Cout]: v = v * s + sh (after bias/res)
+  const float* post_shift = nullptr;
+  int act = ACT_NONE;
+};
+
+// out = act(conv(in0 ++ in1) + bias + res) [* s + sh]
+void conv_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
+                  int stride, int pad, const ConvEpi& epi);
+
+// GroupNorm(G) over a channel-first view, optional FiLM (x*(scale+1)+shift from
+// a [Mtot][NT] table at row offset, column t[b]) then SiLU, optional residual.
+void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, const float* gamma,
+                    const float* beta, const float* film, int film_row, int film_nt, const int* t_batch,
+                    const View* res, double* partials);
+
+// Channel LayerNorm (biased var over C, gamma only; u12:138-147) of in0 ++ in1.
+void channel_ln(hipStream_t s, const View& out, const View& in0, const View* in1, const float* gamma);
+// Fused init_temporal_attn prologue: y = chanLN(x)*g; z = LayerNorm(y)*w+b;
+// writes z and r = x + y (the double residual of u12:915 + 326).
+void temporal_prologue(hipStream_t s, const View& x, const float* gamma, const float* lw, const float* lb,
+                       const View& z, const View& r);
+
+struct AttnGeom {
+  int mode;          // 0 = shifted-window (STW), 1 = temporal (per pixel)
+  int D, H, W;       // unpadded extents
+  int ws0, ws1, ws2; // effective window
+  int ss0, ss1, ss2; // effective shift
+  int Dp, Hp, Wp;    // padded extents
+};
+// qkv: channel-first [B][3*heads*32][T][H][W]; o: [B][heads*32][T][H][W].
+void window_attention(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads,
+                      const float* bias_dense /*[heads][32][32]*/, const float* rope_cos,
+                      const float* rope_sin /*[32][16]*/, float q_scale);
+// TrajWarp cross-attention (u12:719-773): q [B][256][NQ], k,v [B][256][NK].
+void cross_attention(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,
+                     int heads, int NQ, int NK);
+
+void copy_view(hipStream_t s, const View& dst, const View& src);
+void maxpool_hw2(hipStream_t s, const View& dst, const View& src);
+// bilinear (align_corners=False) resize of frames [0,t_split) from a and
+// [t_split,T) from b into dst (u12:1035-1037)
+void bilinear_frames(hipStream_t s, const View& dst, const View& a, const View& b, int t_split);
+// per (b,c) mean and unbiased std (+eps) over T*H*W (u12:670-678)
+void adaptor_stats(hipStream_t s, const View& x, float* mean, float* std_, double* partials);
+void adaptor_normalize(hipStream_t s, const View& dst, const View& src, const float* mean, const float* std_);
+
+// Sampler step kernels.
+struct StepCoef {  // per sampler step (host-computed in fp32 exactly like the reference)
+  float sra, srm1;            // sqrt_recip_alphas_cumprod[t], sqrt_recipm1_alphas_cumprod[t]
+  float c1, c2, sigma;        // DDPM: posterior coef1/coef2, exp(0.5*logvar)*[t!=0]; DDIM: sqrt(a_next), c, sigma
+  int t;                      // model timestep
+  int use_noise;              // 0 => no noise term (DDIM time_next == 0)
+  int kind;                   // 0 = DDPM, 1 = DDIM
+};
+void sampler_step(hipStream_t s, float* x, const float* eps, int B, int n, const StepCoef* coefs,
+                  const int* step_ctr, const float* noise /*[S][B][n] or null*/, uint64_t seed, int sample_base,
+                  int round, int k_lo, int k_hi, float q_w, float* thresh_out);
+void fill_normal(hipStream_t s, float* x, int B, int n, uint64_t seed, int sample_base, int round, int stream_id);
+void set_t_from_step(hipStream_t s, int* t_batch, int B, const StepCoef* coefs, const int* step_ctr);
+void incr_counter(hipStream_t s, int* ctr);
+void t_to_int(hipStream_t s, const int64_t* t, int* t_batch, int B);
+
+// LFAE decoder (no occlusion): flow [B][2][T][h][w] (x,y) -> bilinear to
+// image size, grid_sample(src) (align_corners=True, zeros)
+void warp_frames(hipStream_t s, float* out, const float* src, const float* flow, int B, int C, int T, int S,
+                 int fh, int fw, long out_sb, long out_sc, long out_st);
+
+}  // namespace extdm

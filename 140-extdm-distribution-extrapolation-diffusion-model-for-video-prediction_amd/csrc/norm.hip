@@ -1,0 +1,357 @@
+// Normalisation and layout kernels of the sampling path (all HBM-bound):
+//   GroupNorm(8) + FiLM + SiLU (+ residual)      Block / ResnetBlock, u12:162-203
+//   channel LayerNorm (gamma only, biased var)     LayerNorm/PreNorm,  u12:138-158
+//   fused temporal-attention prologue              u12:306-327, 915
+//   maxpool (1,2,2), bilinear resize, strided copy u12:811, 1035-1037
+//   MotionAdaptor statistics / normalisation       u12:670-691
+// Reductions accumulate in double so the fp32 outputs track the reference's
+// fp32 reductions to rounding.
+#include "kernels.h"
+
+namespace extdm {
+
+namespace {
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Block-wide sum of two doubles (blockDim = 256).
+__device__ __forceinline__ void block_sum2(double& a, double& b, double* sh) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) { sh[w] = a; sh[4 + w] = b; }
+  __syncthreads();
+  a = sh[0] + sh[1] + sh[2] + sh[3];
+  b = sh[4] + sh[5] + sh[6] + sh[7];
+}
+
+struct V5 {
+  const float* p; long sb, sc, st; int C, T, HW;
+};
+
+__device__ __forceinline__ long off5(long sb, long sc, long st, int b, int c, int t, int hw) {
+  return (long)b * sb + (long)c * sc + (long)t * st + hw;
+}
+
+// ---------------- GroupNorm ----------------
+__global__ __launch_bounds__(256) void gn_stats_kernel(const float* __restrict__ x, long sb, long sc, int Cg,
+                                                       int G, long L, int split, double* partials) {
+  const int bg = blockIdx.y;
+  const int b = bg / G, g = bg % G;
+  const float* base = x + (long)b * sb + (long)g * Cg * sc;
+  const long chunk = (L + split - 1) / split;
+  const long e0 = blockIdx.x * chunk;
+  const long e1 = e0 + chunk < L ? e0 + chunk : L;
+  double s = 0.0, ss = 0.0;
+  for (long e = e0 + threadIdx.x; e < e1; e += 256) {
+    const double v = base[e];
+    s += v;
+    ss += v * v;
+  }
+  __shared__ double sh[8];
+  block_sum2(s, ss, sh);
+  if (threadIdx.x == 0) {
+    partials[((long)bg * split + blockIdx.x) * 2] = s;
+    partials[((long)bg * split + blockIdx.x) * 2 + 1] = ss;
+  }
+}
+
+__global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__ x, long sb, long sc,
+                                                       float* out, long osb, long osc, long ost, int C, int Cg,
+                                                       int G, int T, int HW, int split, const double* partials,
+                                                       const float* gamma, const float* beta, const float* film,
+                                                       int film_row, int film_nt, const int* t_batch,
+                                                       const float* res, long rsb, long rsc, long rst,
+                                                       int split2) {
+  const int bg = blockIdx.y;
+  const int b = bg / G, g = bg % G;
+  __shared__ float st[2];
+  if (threadIdx.x == 0) {
+    double s = 0.0, ss = 0.0;
+    for (int i = 0; i < split; ++i) {
+      s += partials[((long)bg * split + i) * 2];
+      ss += partials[((long)bg * split + i) * 2 + 1];
+    }
+    const double n = (double)Cg * T * HW;
+    const double mean = s / n;
+    double var = ss / n - mean * mean;
+    if (var < 0) var = 0;
+    st[0] = (float)mean;
+    st[1] = 1.0f / sqrtf((float)var + 1e-5f);
+  }
+  __syncthreads();
+  const float mean = st[0], rstd = st[1];
+  const long L = (long)Cg * T * HW;
+  const long chunk = (L + split2 - 1) / split2;
+  const long e0 = blockIdx.x * chunk;
+  const long e1 = e0 + chunk < L ? e0 + chunk : L;
+  const float* base = x + (long)b * sb + (long)g * Cg * sc;
+  int tb = film ? t_batch[b] : 0;
+  for (long e = e0 + threadIdx.x; e < e1; e += 256) {
+    const int cl = (int)(e / ((long)T * HW));
+    const int rem = (int)(e - (long)cl * T * HW);
+    const int t = rem / HW, hw = rem - t * HW;
+    const int c = g * Cg + cl;
+    const float sc_ = rstd * gamma[c];
+    const float bi = beta[c] - mean * sc_;
+    float v = base[(long)cl * sc + (long)t * HW + hw] * sc_ + bi;
+    if (film) {
+      const float scale = film[(long)(film_row + c) * film_nt + tb];
+      const float shift = film[(long)(film_row + C + c) * film_nt + tb];
+      v = v * (scale + 1.f) + shift;
+    }
+    v = v / (1.f + expf(-v));
+    if (res) v += res[off5(rsb, rsc, rst, b, c, t, hw)];
+    out[off5(osb, osc, ost, b, c, t, hw)] = v;
+  }
+}
+
+// ---------------- channel LayerNorm ----------------
+__device__ __forceinline__ float ld2(const float* p0, long b0, long c0s, int C0, const float* p1, long b1,
+                                     long c1s, int c) {
+  return c < C0 ? p0[b0 + (long)c * c0s] : p1[b1 + (long)(c - C0) * c1s];
+}
+
+__global__ __launch_bounds__(256) void channel_ln_kernel(float* out, long osb, long osc, long ost,
+                                                         const float* p0, long sb0, long sc0, long st0, int C0,
+                                                         const float* p1, long sb1, long sc1, long st1, int C,
+                                                         int T, int HW, int B, const float* gamma) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long npix = (long)B * T * HW;
+  if (idx >= npix) return;
+  const int hw = (int)(idx % HW);
+  const int t = (int)((idx / HW) % T);
+  const int b = (int)(idx / ((long)HW * T));
+  const long b0 = (long)b * sb0 + (long)t * st0 + hw;
+  const long b1 = (long)b * sb1 + (long)t * st1 + hw;
+  double s = 0.0;
+  for (int c = 0; c < C; ++c) s += ld2(p0, b0, sc0, C0, p1, b1, sc1, c);
+  const double mean = s / C;
+  double v2 = 0.0;
+  for (int c = 0; c < C; ++c) {
+    const double d = ld2(p0, b0, sc0, C0, p1, b1, sc1, c) - mean;
+    v2 += d * d;
+  }
+  const float m = (float)mean;
+  const float den = sqrtf((float)(v2 / C) + 1e-5f);
+  const long ob = (long)b * osb + (long)t * ost + hw;
+  for (int c = 0; c < C; ++c) {
+    const float x = ld2(p0, b0, sc0, C0, p1, b1, sc1, c);
+    out[ob + (long)c * osc] = (x - m) / den * gamma[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void temporal_prologue_kernel(const float* x, long sb, long sc, long st, int C,
+                                                                int T, int HW, int B, const float* gamma,
+                                                                const float* lw, const float* lb, float* z,
+                                                                long zsb, long zsc, long zst, float* r, long rsb,
+                                                                long rsc, long rst) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long npix = (long)B * T * HW;
+  if (idx >= npix) return;
+  const int hw = (int)(idx % HW);
+  const int t = (int)((idx / HW) % T);
+  const int b = (int)(idx / ((long)HW * T));
+  const float* xp = x + (long)b * sb + (long)t * st + hw;
+  double s = 0.0;
+  for (int c = 0; c < C; ++c) s += xp[(long)c * sc];
+  const float m = (float)(s / C);
+  double v2 = 0.0;
+  for (int c = 0; c < C; ++c) {
+    const double d = (double)xp[(long)c * sc] - (double)(s / C);
+    v2 += d * d;
+  }
+  const float den = sqrtf((float)(v2 / C) + 1e-5f);
+  // y = chanLN(x) * gamma ; moments of y
+  double sy = 0.0;
+  for (int c = 0; c < C; ++c) sy += (double)((xp[(long)c * sc] - m) / den * gamma[c]);
+  const double my = sy / C;
+  double vy = 0.0;
+  for (int c = 0; c < C; ++c) {
+    const double d = (double)((xp[(long)c * sc] - m) / den * gamma[c]) - my;
+    vy += d * d;
+  }
+  const float m2 = (float)my;
+  const float rstd2 = 1.0f / sqrtf((float)(vy / C) + 1e-5f);
+  float* zp = z + (long)b * zsb + (long)t * zst + hw;
+  float* rp = r + (long)b * rsb + (long)t * rst + hw;
+  for (int c = 0; c < C; ++c) {
+    const float xv = xp[(long)c * sc];
+    const float y = (xv - m) / den * gamma[c];
+    zp[(long)c * zsc] = (y - m2) * rstd2 * lw[c] + lb[c];
+    rp[(long)c * rsc] = xv + y;
+  }
+}
+
+// ---------------- layout / resampling ----------------
+__global__ __launch_bounds__(256) void copy_kernel(float* d, long dsb, long dsc, long dst_, const float* s,
+                                                   long ssb, long ssc, long sst, int C, int T, int HW, long total) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int hw = (int)(idx % HW);
+  long r = idx / HW;
+  const int t = (int)(r % T); r /= T;
+  const int c = (int)(r % C);
+  const int b = (int)(r / C);
+  d[off5(dsb, dsc, dst_, b, c, t, hw)] = s[off5(ssb, ssc, sst, b, c, t, hw)];
+}
+
+__global__ __launch_bounds__(256) void maxpool_kernel(float* d, long dsb, long dsc, long dst_, const float* s,
+                                                      long ssb, long ssc, long sst, int C, int T, int Ho, int Wo,
+                                                      int Wi, long total) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int x = (int)(idx % Wo);
+  long r = idx / Wo;
+  const int y = (int)(r % Ho); r /= Ho;
+  const int t = (int)(r % T); r /= T;
+  const int c = (int)(r % C);
+  const int b = (int)(r / C);
+  const float* p = s + off5(ssb, ssc, sst, b, c, t, 0) + (long)(2 * y) * Wi + 2 * x;
+  const float v = fmaxf(fmaxf(p[0], p[1]), fmaxf(p[Wi], p[Wi + 1]));
+  d[off5(dsb, dsc, dst_, b, c, t, y * Wo + x)] = v;
+}
+
+// torch upsample_bilinear2d, align_corners=False, scale = in/out
+__device__ __forceinline__ void lin_idx(int o, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  const float scale = (float)in / (float)out;
+  float src = scale * ((float)o + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = src - (float)i0;
+  l0 = 1.f - l1;
+}
+
+__global__ __launch_bounds__(256) void bilinear_kernel(float* d, long dsb, long dsc, long dst_, const float* a,
+                                                       long asb, long asc, long ast, const float* bb, long bsb,
+                                                       long bsc, long bst, int tsplit, int C, int T, int Ho,
+                                                       int Wo, int Hi, int Wi, long total) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int x = (int)(idx % Wo);
+  long r = idx / Wo;
+  const int y = (int)(r % Ho); r /= Ho;
+  const int t = (int)(r % T); r /= T;
+  const int c = (int)(r % C);
+  const int b = (int)(r / C);
+  const float* p = t < tsplit ? a + off5(asb, asc, ast, b, c, t, 0) : bb + off5(bsb, bsc, bst, b, c, t - tsplit, 0);
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  lin_idx(y, Hi, Ho, y0, y1, ly0, ly1);
+  lin_idx(x, Wi, Wo, x0, x1, lx0, lx1);
+  const float v = ly0 * (lx0 * p[y0 * Wi + x0] + lx1 * p[y0 * Wi + x1]) +
+                  ly1 * (lx0 * p[y1 * Wi + x0] + lx1 * p[y1 * Wi + x1]);
+  d[off5(dsb, dsc, dst_, b, c, t, y * Wo + x)] = v;
+}
+
+// ---------------- MotionAdaptor ----------------
+__global__ __launch_bounds__(256) void adaptor_stats_kernel(const float* x, long sb, long sc, long st, int C, int T,
+                                                            int HW, float* mean_out, float* std_out) {
+  const int bc = blockIdx.x;
+  const int b = bc / C, c = bc % C;
+  const float* p = x + (long)b * sb + (long)c * sc;
+  const int n = T * HW;
+  double s = 0.0, dummy = 0.0;
+  for (int e = threadIdx.x; e < n; e += 256) s += p[(long)(e / HW) * st + e % HW];
+  __shared__ double sh[8];
+  block_sum2(s, dummy, sh);
+  const double mean = s / n;
+  double v2 = 0.0;
+  dummy = 0.0;
+  for (int e = threadIdx.x; e < n; e += 256) {
+    const double d = p[(long)(e / HW) * st + e % HW] - mean;
+    v2 += d * d;
+  }
+  __syncthreads();
+  block_sum2(v2, dummy, sh);
+  if (threadIdx.x == 0) {
+    mean_out[bc] = (float)mean;
+    std_out[bc] = sqrtf((float)(v2 / (n - 1)) + 1e-5f);
+  }
+}
+
+__global__ __launch_bounds__(256) void adaptor_norm_kernel(float* d, long dsb, long dsc, long dst_, const float* s,
+                                                           long ssb, long ssc, long sst, int C, int T, int HW,
+                                                           const float* mean, const float* std_, long total) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int hw = (int)(idx % HW);
+  long r = idx / HW;
+  const int t = (int)(r % T); r /= T;
+  const int c = (int)(r % C);
+  const int b = (int)(r / C);
+  d[off5(dsb, dsc, dst_, b, c, t, hw)] = (s[off5(ssb, ssc, sst, b, c, t, hw)] - mean[b * C + c]) / std_[b * C + c];
+}
+
+inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, const float* gamma,
+                    const float* beta, const float* film, int film_row, int film_nt, const int* t_batch,
+                    const View* res, double* partials) {
+  const int Cg = x.C / groups;
+  const long L = (long)Cg * x.T * x.HW();
+  int split = (int)((L + 32767) / 32768);
+  if (split < 1) split = 1;
+  if (split > 64) split = 64;
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(split, x.B * groups), dim3(256), 0, s, x.p, x.sb, x.sc, Cg, groups, L,
+                     split, partials);
+  int split2 = (int)((L + 8191) / 8192);
+  if (split2 < 1) split2 = 1;
+  hipLaunchKernelGGL(gn_apply_kernel, dim3(split2, x.B * groups), dim3(256), 0, s, x.p, x.sb, x.sc, out.p, out.sb,
+                     out.sc, out.st, x.C, Cg, groups, x.T, x.HW(), split, partials, gamma, beta, film, film_row,
+                     film_nt, t_batch, res ? res->p : nullptr, res ? res->sb : 0, res ? res->sc : 0,
+                     res ? res->st : 0, split2);
+}
+
+void channel_ln(hipStream_t s, const View& out, const View& in0, const View* in1, const float* gamma) {
+  const View& i1 = in1 ? *in1 : in0;
+  const long npix = (long)out.B * out.T * out.HW();
+  hipLaunchKernelGGL(channel_ln_kernel, dim3(nblk(npix)), dim3(256), 0, s, out.p, out.sb, out.sc, out.st, in0.p,
+                     in0.sb, in0.sc, in0.st, in0.C, i1.p, i1.sb, i1.sc, i1.st, out.C, out.T, out.HW(), out.B, gamma);
+}
+
+void temporal_prologue(hipStream_t s, const View& x, const float* gamma, const float* lw, const float* lb,
+                       const View& z, const View& r) {
+  const long npix = (long)x.B * x.T * x.HW();
+  hipLaunchKernelGGL(temporal_prologue_kernel, dim3(nblk(npix)), dim3(256), 0, s, x.p, x.sb, x.sc, x.st, x.C, x.T,
+                     x.HW(), x.B, gamma, lw, lb, z.p, z.sb, z.sc, z.st, r.p, r.sb, r.sc, r.st);
+}
+
+void copy_view(hipStream_t s, const View& d, const View& src) {
+  const long total = d.numel();
+  hipLaunchKernelGGL(copy_kernel, dim3(nblk(total)), dim3(256), 0, s, d.p, d.sb, d.sc, d.st, src.p, src.sb, src.sc,
+                     src.st, d.C, d.T, d.HW(), total);
+}
+
+void maxpool_hw2(hipStream_t s, const View& d, const View& src) {
+  const long total = d.numel();
+  hipLaunchKernelGGL(maxpool_kernel, dim3(nblk(total)), dim3(256), 0, s, d.p, d.sb, d.sc, d.st, src.p, src.sb,
+                     src.sc, src.st, d.C, d.T, d.H, d.W, src.W, total);
+}
+
+void bilinear_frames(hipStream_t s, const View& d, const View& a, const View& b, int t_split) {
+  const long total = d.numel();
+  hipLaunchKernelGGL(bilinear_kernel, dim3(nblk(total)), dim3(256), 0, s, d.p, d.sb, d.sc, d.st, a.p, a.sb, a.sc,
+                     a.st, b.p, b.sb, b.sc, b.st, t_split, d.C, d.T, d.H, d.W, a.H, a.W, total);
+}
+
+void adaptor_stats(hipStream_t s, const View& x, float* mean, float* std_, double* /*partials*/) {
+  hipLaunchKernelGGL(adaptor_stats_kernel, dim3(x.B * x.C), dim3(256), 0, s, x.p, x.sb, x.sc, x.st, x.C, x.T, x.HW(),
+                     mean, std_);
+}
+
+void adaptor_normalize(hipStream_t s, const View& d, const View& src, const float* mean, const float* std_) {
+  const long total = d.numel();
+  hipLaunchKernelGGL(adaptor_norm_kernel, dim3(nblk(total)), dim3(256), 0, s, d.p, d.sb, d.sc, d.st, src.p, src.sb,
+                     src.sc, src.st, d.C, d.T, d.HW(), mean, std_, total);
+}
+
+}  // namespace extdm

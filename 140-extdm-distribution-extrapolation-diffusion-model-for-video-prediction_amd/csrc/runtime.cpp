@@ -1,0 +1,836 @@
+// ExtDM sampling runtime: weight registry and packing, t-only tables, the
+// u12 Unet3D forward as a sequence of HIP kernel launches over a stack-arena
+// workspace, the sampler loop replayed from one captured hipGraph step, and
+// the C ABI of include/extdm.h.
+//
+// Forward structure follows Unet3D.forward (DenoiseNet_..._u12.py:1017-1086);
+// each helper cites the reference block it implements.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "extdm.h"
+#include "kernels.h"
+
+using namespace extdm;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess)                                                                  \
+      throw Error(std::string(#x) + " failed: " + hipGetErrorString(e_) + " @" + std::to_string(__LINE__)); \
+  } while (0)
+
+#define REQUIRE(c, msg) \
+  do {                  \
+    if (!(c)) throw Error(msg); \
+  } while (0)
+
+struct HostTensor {
+  std::vector<float> f;
+  std::vector<int64_t> i;
+  std::vector<int64_t> shape;
+  bool is_int = false;
+};
+
+// Stack allocator over one device allocation. In planning mode it only
+// measures the peak so the workspace can be sized exactly.
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0, top = 0, peak = 0;
+  bool planning = false;
+  float* alloc(size_t nfloat) {
+    const size_t bytes = (nfloat * sizeof(float) + 255) & ~size_t(255);
+    const size_t off = top;
+    top += bytes;
+    peak = std::max(peak, top);
+    if (planning) return reinterpret_cast<float*>(uintptr_t(0x100000) + off);
+    if (top > cap) throw Error("workspace overflow (batch larger than max_batch?)");
+    return reinterpret_cast<float*>(base + off);
+  }
+  size_t mark() const { return top; }
+  void release(size_t m) { top = m; }
+};
+
+struct Scope {
+  Arena& a;
+  size_t m;
+  explicit Scope(Arena& ar) : a(ar), m(ar.mark()) {}
+  ~Scope() { a.release(m); }
+};
+
+struct AdaptorGeom {
+  int L, F;
+};
+
+}  // namespace
+
+struct ExtdmHandle {
+  ExtdmConfig cfg{};
+  std::unordered_map<std::string, HostTensor> host;
+  std::unordered_map<std::string, float*> dev;      // raw fp32 tensors on device
+  std::unordered_map<std::string, PackedW> packed;  // GEMM-packed conv / linear weights
+  std::vector<void*> allocations;
+  bool finalized = false;
+  bool plan = false;
+
+  // t-only tables
+  float* film = nullptr;  // [Mtot][NT]
+  int film_nt = 0;
+  std::unordered_map<std::string, int> film_row;
+  float* rope_cos = nullptr;  // [32][16]
+  float* rope_sin = nullptr;
+  std::unordered_map<std::string, float*> bias_dense;  // STW layer prefix -> [heads][32][32]
+  float* time_bias = nullptr;                            // [heads][32][32]
+
+  // workspace
+  Arena arena;
+  double* partials = nullptr;
+  int* t_batch = nullptr;
+  int* step_ctr = nullptr;
+  StepCoef* coefs = nullptr;
+  int coefs_cap = 0;
+  float* eps_buf = nullptr;
+  hipStream_t work = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+
+  hipStream_t s = nullptr;  // stream of the current call
+
+  // ------------------------------------------------------------------ utils
+  float* dmalloc(size_t bytes) {
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, bytes));
+    allocations.push_back(p);
+    return reinterpret_cast<float*>(p);
+  }
+  const HostTensor& H(const std::string& n) const {
+    auto it = host.find(n);
+    if (it == host.end()) throw Error("missing weight: " + n);
+    return it->second;
+  }
+  bool has(const std::string& n) const { return host.count(n) != 0; }
+  float* D(const std::string& n) {
+    auto it = dev.find(n);
+    if (it != dev.end()) return it->second;
+    const HostTensor& t = H(n);
+    REQUIRE(!t.is_int, "expected float tensor: " + n);
+    float* p = dmalloc(t.f.size() * sizeof(float));
+    HIPCHK(hipMemcpy(p, t.f.data(), t.f.size() * sizeof(float), hipMemcpyHostToDevice));
+    dev[n] = p;
+    return p;
+  }
+
+  // Pack a conv weight W[co][ci][(kt)][kh][kw] (or linear W[co][ci]) as
+  // A[k][m], k = ci*kh*kw + ky*kw + kx, zero padded.
+  const PackedW& P(const std::string& n) {
+    auto it = packed.find(n);
+    if (it != packed.end()) return it->second;
+    const HostTensor& t = H(n);
+    const auto& sh = t.shape;
+    PackedW pw;
+    int co = (int)sh[0], ci = (int)sh[1];
+    int kh = 1, kw = 1;
+    if (sh.size() >= 4) { kh = (int)sh[sh.size() - 2]; kw = (int)sh[sh.size() - 1]; }
+    pw.M = co; pw.K = ci * kh * kw; pw.KH = kh; pw.KW = kw;
+    const int bm = conv_bm(co);
+    pw.Mpad = (co + bm - 1) / bm * bm;
+    pw.Kpad = (pw.K + 15) / 16 * 16;
+    std::vector<float> a((size_t)pw.Kpad * pw.Mpad, 0.f);
+    for (int m = 0; m < co; ++m)
+      for (int k = 0; k < pw.K; ++k) a[(size_t)k * pw.Mpad + m] = t.f[(size_t)m * pw.K + k];
+    pw.w = dmalloc(a.size() * sizeof(float));
+    HIPCHK(hipMemcpy(pw.w, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
+    return packed[n] = pw;
+  }
+  // ConvTranspose3d(1,4,4)/s2/p1 weight W[ci][co][1][4][4] -> four 2x2 parity GEMMs:
+  // parity (py,px) tap (ky',kx') uses W[..][3-py-2ky'][3-px-2kx'].
+  const PackedW& Pdeconv(const std::string& n) {
+    auto it = packed.find(n);
+    if (it != packed.end()) return it->second;
+    const HostTensor& t = H(n);
+    const int ci = (int)t.shape[0], co = (int)t.shape[1];
+    REQUIRE(t.shape[3] == 4 && t.shape[4] == 4, "deconv expects (1,4,4) kernels: " + n);
+    PackedW pw;
+    pw.M = co; pw.K = ci * 4; pw.KH = 2; pw.KW = 2; pw.mode = MODE_DECONV;
+    const int bm = conv_bm(co);
+    pw.Mpad = (co + bm - 1) / bm * bm;
+    pw.Kpad = (pw.K + 15) / 16 * 16;
+    const size_t plane = (size_t)pw.Kpad * pw.Mpad;
+    std::vector<float> a(4 * plane, 0.f);
+    for (int par = 0; par < 4; ++par) {
+      const int py = par >> 1, px = par & 1;
+      for (int c = 0; c < ci; ++c)
+        for (int ky = 0; ky < 2; ++ky)
+          for (int kx = 0; kx < 2; ++kx) {
+            const int k = c * 4 + ky * 2 + kx;
+            const int sy = 3 - py - 2 * ky, sx = 3 - px - 2 * kx;
+            for (int m = 0; m < co; ++m)
+              a[par * plane + (size_t)k * pw.Mpad + m] = t.f[(((size_t)c * co + m) * 4 + sy) * 4 + sx];
+          }
+    }
+    pw.w = dmalloc(a.size() * sizeof(float));
+    HIPCHK(hipMemcpy(pw.w, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
+    return packed[n] = pw;
+  }
+  PackedW pack_matrix(const std::vector<float>& wrow /*[M][K]*/, int M, int K) {
+    PackedW pw;
+    pw.M = M; pw.K = K;
+    const int bm = conv_bm(M);
+    pw.Mpad = (M + bm - 1) / bm * bm;
+    pw.Kpad = (K + 15) / 16 * 16;
+    std::vector<float> a((size_t)pw.Kpad * pw.Mpad, 0.f);
+    for (int m = 0; m < M; ++m)
+      for (int k = 0; k < K; ++k) a[(size_t)k * pw.Mpad + m] = wrow[(size_t)m * K + k];
+    pw.w = dmalloc(a.size() * sizeof(float));
+    HIPCHK(hipMemcpy(pw.w, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
+    return pw;
+  }
+
+  View alloc_cf(int B, int C, int T, int Hh, int Ww) {
+    return cf_view(arena.alloc((size_t)B * C * T * Hh * Ww), B, C, T, Hh, Ww);
+  }
+  View alloc_tm(int B, int C, int T, int Hh, int Ww) {
+    return tm_view(arena.alloc((size_t)B * C * T * Hh * Ww), B, C, T, Hh, Ww);
+  }
+
+  // ---------------------------------------------------------------- op shims
+  void conv(const View& out, const View& in0, const View* in1, const PackedW& w, int stride, int pad,
+            const float* bias, const View* res = nullptr, int act = ACT_NONE, const float* ps = nullptr,
+            const float* psh = nullptr) {
+    REQUIRE((in1 ? in0.C + in1->C : in0.C) * w.KH * w.KW == w.K || w.mode == MODE_DECONV,
+            "conv: input channels do not match the weight");
+    REQUIRE(out.C == w.M, "conv: output channels do not match the weight");
+    if (plan) return;
+    ConvEpi e;
+    e.bias = bias;
+    if (res) { e.res = res->p; e.res_sb = res->sb; e.res_sc = res->sc; e.res_st = res->st; }
+    e.act = act;
+    e.post_scale = ps;
+    e.post_shift = psh;
+    conv_forward(s, out, in0, in1, w, stride, pad, e);
+  }
+
+  // ----------------------------------------------------------- Unet blocks
+  // ResnetBlock (u12:181-203): block1 (conv, GN, FiLM, SiLU), block2, + res_conv / identity
+  void resblock(const std::string& p, const View& in0, const View* in1, const View& out) {
+    Scope sc(arena);
+    const int B = out.B, C = out.C, T = out.T, Hh = out.H, Ww = out.W;
+    View h1 = alloc_cf(B, C, T, Hh, Ww);
+    conv(h1, in0, in1, P(p + ".block1.proj.weight"), 1, 1, D(p + ".block1.proj.bias"));
+    const bool has_mlp = film_row.count(p) != 0;
+    if (!plan)
+      groupnorm_silu(s, h1, h1, 8, D(p + ".block1.norm.weight"), D(p + ".block1.norm.bias"),
+                     has_mlp ? film : nullptr, has_mlp ? film_row[p] : 0, film_nt, t_batch, nullptr, partials);
+    View h2 = alloc_cf(B, C, T, Hh, Ww);
+    conv(h2, h1, nullptr, P(p + ".block2.proj.weight"), 1, 1, D(p + ".block2.proj.bias"));
+    if (has(p + ".res_conv.weight")) {
+      if (!plan)
+        groupnorm_silu(s, h2, h2, 8, D(p + ".block2.norm.weight"), D(p + ".block2.norm.bias"), nullptr, 0, 0,
+                       nullptr, nullptr, partials);
+      conv(out, in0, in1, P(p + ".res_conv.weight"), 1, 0, D(p + ".res_conv.bias"), &h2);
+    } else {
+      REQUIRE(in1 == nullptr && in0.C == C, "identity residual needs matching channels");
+      if (!plan)
+        groupnorm_silu(s, h2, out, 8, D(p + ".block2.norm.weight"), D(p + ".block2.norm.bias"), nullptr, 0, 0,
+                       nullptr, &in0, partials);
+    }
+  }
+
+  AttnGeom stw_geom(int Dd, int Hh, int Ww, bool shifted) const {
+    // get_window_size (u12:392-405) + padding (u12:525-535)
+    AttnGeom g{};
+    g.mode = 0;
+    g.D = Dd; g.H = Hh; g.W = Ww;
+    int ws[3] = {cfg.window[0], cfg.window[1], cfg.window[2]};
+    int ss[3] = {shifted ? cfg.window[0] / 2 : 0, shifted ? cfg.window[1] / 2 : 0, shifted ? cfg.window[2] / 2 : 0};
+    const int ext[3] = {Dd, Hh, Ww};
+    for (int i = 0; i < 3; ++i)
+      if (ext[i] <= ws[i]) { ws[i] = ext[i]; ss[i] = 0; }
+    g.ws0 = ws[0]; g.ws1 = ws[1]; g.ws2 = ws[2];
+    g.ss0 = ss[0]; g.ss1 = ss[1]; g.ss2 = ss[2];
+    g.Dp = (Dd + ws[0] - 1) / ws[0] * ws[0];
+    g.Hp = (Hh + ws[1] - 1) / ws[1] * ws[1];
+    g.Wp = (Ww + ws[2] - 1) / ws[2] * ws[2];
+    return g;
+  }
+
+  // Residual(PreNorm(STWAttentionLayer)) in place on x (u12:498-559, 961-963)
+  void stw(const std::string& p, const View& x, bool shifted) {
+    Scope sc(arena);
+    const int hid = cfg.heads * 32;
+    View ln = alloc_cf(x.B, x.C, x.T, x.H, x.W);
+    if (!plan) channel_ln(s, ln, x, nullptr, D(p + ".fn.norm.gamma"));
+    View qkv = alloc_cf(x.B, 3 * hid, x.T, x.H, x.W);
+    conv(qkv, ln, nullptr, P(p + ".fn.fn.attn.qkv.weight"), 1, 0, nullptr);
+    View o = alloc_cf(x.B, hid, x.T, x.H, x.W);
+    const AttnGeom g = stw_geom(x.T, x.H, x.W, shifted);
+    if (!plan)
+      window_attention(s, qkv, o, g, cfg.heads, bias_dense.at(p), rope_cos, rope_sin,
+                       1.0f / std::sqrt((float)cfg.dim_head));
+    conv(x, o, nullptr, P(p + ".fn.fn.attn.proj.weight"), 1, 0, D(p + ".fn.fn.attn.proj.bias"), &x);
+  }
+
+  AdaptorGeom adaptor_geom() const {
+    const int L = std::max(1, (int)std::ceil(std::log2((double)(cfg.tp + 1) / cfg.tc)));
+    return {L, ((1 << L) - 1) * cfg.tc};
+  }
+
+  // MotionAdaptor in place on frames [tc, T) of x (u12:644-717)
+  void adaptor(const std::string& p, const View& x) {
+    Scope sc(arena);
+    const int B = x.B, C = x.C, Hh = x.H, Ww = x.W, tc = cfg.tc, tp = cfg.tp, HW = Hh * Ww;
+    const AdaptorGeom ag = adaptor_geom();
+    const std::string ap = p + ".adaptors";
+    View E = alloc_tm(B, C, tc << ag.L, Hh, Ww);
+    {
+      Scope s2(arena);
+      View ln = alloc_cf(B, C, tc, Hh, Ww);
+      View xm = x.frames(0, tc);
+      if (!plan) channel_ln(s, ln, xm, nullptr, D(ap + ".predictor.fn.norm.gamma"));
+      conv(E.frames(0, tc), ln, nullptr, P(ap + ".predictor.fn.fn.weight"), 1, 0, D(ap + ".predictor.fn.fn.bias"),
+           &xm);
+    }
+    for (int l = 0; l < ag.L; ++l) {
+      Scope s2(arena);
+      const int nl = tc << l;
+      float* mean = arena.alloc((size_t)B * C);
+      float* sd = arena.alloc((size_t)B * C);
+      View cur = E.frames(0, nl);
+      if (!plan) adaptor_stats(s, cur, mean, sd, partials);
+      View hn = alloc_tm(B, C, nl, Hh, Ww);
+      if (!plan) adaptor_normalize(s, hn, cur, mean, sd);
+      conv(E.frames(nl, nl), hn, nullptr, P(ap + ".extrapolators." + std::to_string(l) + ".fn.weight"), 1, 1,
+           nullptr, &hn, ACT_NONE, sd, mean);
+    }
+    // Tmodulator: 1x1 conv over '(T C)' channels of the F extrapolated frames
+    View ein = E.frames(tc, ag.F);
+    ein.C = ag.F * C; ein.T = 1; ein.sc = HW; ein.st = 0;
+    View mo = alloc_tm(B, C, tp, Hh, Ww);
+    View mo2 = mo;
+    mo2.C = tp * C; mo2.T = 1; mo2.sc = HW; mo2.st = 0;
+    conv(mo2, ein, nullptr, P(p + ".Tmodulator.weight"), 1, 0, D(p + ".Tmodulator.bias"));
+    // fuser: PreNorm(2C, conv1x1) on cat([xm2p, xp]) + xp
+    View xp = x.frames(tc, tp);
+    View lnf = alloc_cf(B, 2 * C, tp, Hh, Ww);
+    if (!plan) channel_ln(s, lnf, mo, &xp, D(p + ".fuser.norm.gamma"));
+    conv(xp, lnf, nullptr, P(p + ".fuser.fn.weight"), 1, 0, D(p + ".fuser.fn.bias"), &xp);
+  }
+
+  // TrajWarp (u12:804-827) -> the fused pred-frame features fp' [B,256,tp,fs,fs]
+  void trajwarp(const View& x0, const View& fea, const View& fp_out) {
+    Scope sc(arena);
+    const int B = x0.B, C = fea.C, tc = cfg.tc, tp = cfg.tp, fs = cfg.fea_size;
+    REQUIRE(x0.H / 2 == fs && x0.W / 2 == fs, "TrajWarp: maxpooled latent must match cond_fea size");
+    View xq = alloc_cf(B, x0.C, tp, fs, fs);
+    if (!plan) maxpool_hw2(s, xq, x0.frames(tc, tp));
+    const std::string c = "init_traj.cross_att";
+    View q = alloc_cf(B, C, tp, fs, fs), k = alloc_cf(B, C, tc, fs, fs), v = alloc_cf(B, C, tc, fs, fs);
+    conv(q, xq, nullptr, P(c + ".linear_q.weight"), 1, 0, D(c + ".linear_q.bias"), nullptr, ACT_RELU);
+    View fm = fea.frames(0, tc);
+    conv(k, fm, nullptr, P(c + ".linear_k.weight"), 1, 0, D(c + ".linear_k.bias"), nullptr, ACT_RELU);
+    conv(v, fm, nullptr, P(c + ".linear_v.weight"), 1, 0, D(c + ".linear_v.bias"), nullptr, ACT_RELU);
+    View a = alloc_cf(B, C, tp, fs, fs);
+    if (!plan) cross_attention(s, q.p, k.p, v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
+    View fm2p = alloc_cf(B, C, tp, fs, fs);
+    conv(fm2p, a, nullptr, P(c + ".linear_o.weight"), 1, 0, D(c + ".linear_o.bias"), nullptr, ACT_RELU);
+    View fp = fea.frames(tc, tp);
+    conv(fp_out, fp, &fm2p, P("init_traj.fuser.weight"), 1, 0, D("init_traj.fuser.bias"));
+  }
+
+  // Unet3D.forward (u12:1017-1086). x: [B,3,tp,L,L], cond: [B,3,tc,L,L],
+  // fea: [B,fea_ch,T,fs,fs], eps: [B,3,tp,L,L]; t_batch already on device.
+  void unet_forward(int B, const float* x, const float* cond, const float* fea, float* eps) {
+    Scope top(arena);
+    const int tc = cfg.tc, tp = cfg.tp, T = tc + tp, L = cfg.latent, fs = cfg.fea_size, d0 = cfg.dim;
+    View vx = cf_view(const_cast<float*>(x), B, 3, tp, L, L);
+    View vc = cf_view(const_cast<float*>(cond), B, 3, tc, L, L);
+    View vf = cf_view(const_cast<float*>(fea), B, cfg.fea_ch, T, fs, fs);
+    View veps = cf_view(eps, B, 3, tp, L, L);
+
+    View r = alloc_cf(B, d0, T, L, L);  // `r` of u12:1042
+    {
+      Scope sc(arena);
+      View xin = alloc_cf(B, 3, T, L, L);
+      if (!plan) { copy_view(s, xin.frames(0, tc), vc); copy_view(s, xin.frames(tc, tp), vx); }
+      View x0 = alloc_cf(B, 256, T, L, L);
+      conv(x0, xin, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
+      View fp2 = alloc_cf(B, cfg.fea_ch, tp, fs, fs);
+      trajwarp(x0, vf, fp2);
+      View fup = alloc_cf(B, cfg.fea_ch, T, L, L);
+      if (!plan) bilinear_frames(s, fup, vf, fp2, tc);
+      conv(r, x0, &fup, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+    }
+    // init_temporal_attn (u12:903-915, 236-327)
+    View xt = alloc_cf(B, d0, T, L, L);
+    {
+      Scope sc(arena);
+      const std::string a = "init_temporal_attn.fn.fn.fn";
+      const int hid = cfg.heads * 32;
+      View z = alloc_cf(B, d0, T, L, L), rr = alloc_cf(B, d0, T, L, L);
+      if (!plan)
+        temporal_prologue(s, r, D("init_temporal_attn.fn.norm.gamma"), D(a + ".norm.weight"), D(a + ".norm.bias"), z,
+                          rr);
+      View qkv = alloc_cf(B, 3 * hid, T, L, L);
+      conv(qkv, z, nullptr, P(a + ".attn.to_qkv.weight"), 1, 0, nullptr);
+      View o = alloc_cf(B, hid, T, L, L);
+      AttnGeom g{};
+      g.mode = 1; g.D = T; g.H = L; g.W = L;
+      if (!plan)
+        window_attention(s, qkv, o, g, cfg.heads, time_bias, rope_cos, rope_sin, 1.0f / std::sqrt((float)cfg.dim_head));
+      conv(xt, o, nullptr, P(a + ".attn.to_out.weight"), 1, 0, nullptr, &rr);
+    }
+    // downs
+    std::vector<int> dims = {d0};
+    for (int i = 0; i < cfg.n_levels; ++i) dims.push_back(d0 * cfg.dim_mults[i]);
+    const int nl = cfg.n_levels;
+    std::vector<View> skips;
+    View cur = xt;
+    int Hc = L;
+    for (int i = 0; i < nl; ++i) {
+      const std::string p = "downs." + std::to_string(i);
+      const int dout = dims[i + 1];
+      View a1 = alloc_cf(B, dout, T, Hc, Hc);
+      resblock(p + ".0", cur, nullptr, a1);
+      stw(p + ".1", a1, true);
+      View a2 = alloc_cf(B, dout, T, Hc, Hc);
+      resblock(p + ".2", a1, nullptr, a2);
+      stw(p + ".3", a2, false);
+      if (i > 1) adaptor(p + ".4", a2);
+      skips.push_back(a2);
+      if (i < nl - 1) {
+        View dn = alloc_cf(B, dout, T, Hc / 2, Hc / 2);
+        conv(dn, a2, nullptr, P(p + ".5.weight"), 2, 1, D(p + ".5.bias"));
+        cur = dn;
+        Hc /= 2;
+      } else {
+        cur = a2;
+      }
+    }
+    // mid (u12:1068-1072)
+    {
+      const int md = dims[nl];
+      View m1 = alloc_cf(B, md, T, Hc, Hc);
+      resblock("mid_block1", cur, nullptr, m1);
+      stw("mid_attn1", m1, true);
+      View m2 = alloc_cf(B, md, T, Hc, Hc);
+      resblock("mid_block2", m1, nullptr, m2);
+      stw("mid_attn2", m2, false);
+      adaptor("mid_adaptor", m2);
+      cur = m2;
+    }
+    // ups (u12:1074-1081)
+    for (int i = 0; i < nl; ++i) {
+      const std::string p = "ups." + std::to_string(i);
+      const int din = dims[nl - 1 - i];
+      View skip = skips.back();
+      skips.pop_back();
+      View u1 = alloc_cf(B, din, T, Hc, Hc);
+      resblock(p + ".0", cur, &skip, u1);
+      stw(p + ".1", u1, true);
+      View u2 = alloc_cf(B, din, T, Hc, Hc);
+      resblock(p + ".2", u1, nullptr, u2);
+      stw(p + ".3", u2, false);
+      if (i > 1) adaptor(p + ".4", u2);
+      if (i < nl - 1) {
+        View up = alloc_cf(B, din, T, Hc * 2, Hc * 2);
+        conv(up, u2, nullptr, Pdeconv(p + ".5.weight"), 1, 0, D(p + ".5.bias"));
+        cur = up;
+        Hc *= 2;
+      } else {
+        cur = u2;
+      }
+    }
+    // heads (u12:1083-1086): final_conv -> flow (2), occlusion_map -> 1, frames tc:
+    {
+      Scope sc(arena);
+      View g = alloc_cf(B, d0, T, L, L);
+      resblock("final_conv.0", cur, &r, g);
+      conv(veps.chans(0, 2), g.frames(tc, tp), nullptr, P("final_conv.1.weight"), 1, 0, D("final_conv.1.bias"));
+      View o = alloc_cf(B, d0, T, L, L);
+      resblock("occlusion_map.0", cur, &r, o);
+      conv(veps.chans(2, 1), o.frames(tc, tp), nullptr, P("occlusion_map.1.weight"), 1, 0,
+           D("occlusion_map.1.bias"));
+    }
+  }
+
+  // ------------------------------------------------------------ finalize
+  void build_tables() {
+    const int NT = cfg.timesteps;
+    film_nt = NT;
+    const int dim = cfg.dim, half = dim / 2, tdim = dim * 4;
+    // sinusoidal embedding of every t (SinusoidalPosEmb, u12:109-121) as [dim][NT]
+    std::vector<float> sinus((size_t)dim * NT);
+    const float es = (float)(std::log(10000.0) / (half - 1));
+    for (int i = 0; i < half; ++i) {
+      const float f = std::exp((float)i * -es);
+      for (int t = 0; t < NT; ++t) {
+        const float a = (float)t * f;
+        sinus[(size_t)i * NT + t] = std::sin(a);
+        sinus[(size_t)(half + i) * NT + t] = std::cos(a);
+      }
+    }
+    float* d_sin = dmalloc(sinus.size() * sizeof(float));
+    HIPCHK(hipMemcpy(d_sin, sinus.data(), sinus.size() * sizeof(float), hipMemcpyHostToDevice));
+    float* h1 = dmalloc((size_t)tdim * NT * sizeof(float));
+    float* te = dmalloc((size_t)tdim * NT * sizeof(float));
+    View vs = cf_view(d_sin, 1, dim, 1, 1, NT);
+    View vh1 = cf_view(h1, 1, tdim, 1, 1, NT);
+    View vte = cf_view(te, 1, tdim, 1, 1, NT);
+    // time_mlp: Linear -> GELU -> Linear; the ResnetBlock mlps start with SiLU (u12:184-187)
+    conv(vh1, vs, nullptr, P("time_mlp.1.weight"), 1, 0, D("time_mlp.1.bias"), nullptr, ACT_GELU);
+    conv(vte, vh1, nullptr, P("time_mlp.3.weight"), 1, 0, D("time_mlp.3.bias"), nullptr, ACT_SILU);
+    // all ResnetBlock FiLM projections in one GEMM
+    std::vector<std::string> blocks;
+    for (auto& kv : host) {
+      const std::string& n = kv.first;
+      const std::string suf = ".mlp.1.weight";
+      if (n.size() > suf.size() && n.compare(n.size() - suf.size(), suf.size(), suf) == 0)
+        blocks.push_back(n.substr(0, n.size() - suf.size()));
+    }
+    std::sort(blocks.begin(), blocks.end());
+    int mtot = 0;
+    for (auto& b : blocks) { film_row[b] = mtot; mtot += (int)H(b + ".mlp.1.weight").shape[0]; }
+    std::vector<float> wcat((size_t)mtot * tdim), bcat(mtot);
+    for (auto& b : blocks) {
+      const HostTensor& w = H(b + ".mlp.1.weight");
+      const HostTensor& bb = H(b + ".mlp.1.bias");
+      std::copy(w.f.begin(), w.f.end(), wcat.begin() + (size_t)film_row[b] * tdim);
+      std::copy(bb.f.begin(), bb.f.end(), bcat.begin() + film_row[b]);
+    }
+    if (mtot > 0) {
+      PackedW pw = pack_matrix(wcat, mtot, tdim);
+      float* dbias = dmalloc(bcat.size() * sizeof(float));
+      HIPCHK(hipMemcpy(dbias, bcat.data(), bcat.size() * sizeof(float), hipMemcpyHostToDevice));
+      film = dmalloc((size_t)mtot * NT * sizeof(float));
+      conv(cf_view(film, 1, mtot, 1, 1, NT), vte, nullptr, pw, 1, 0, dbias);
+    }
+    // rotary tables (rotary-embedding-torch 0.8.3): angle = pos * freqs[i]
+    {
+      const HostTensor& fr = H("init_temporal_attn.fn.fn.fn.attn.rotary_emb.freqs");
+      REQUIRE(fr.f.size() == 16, "rotary freqs: dim_head 32 expected");
+      std::vector<float> c(32 * 16), sn(32 * 16);
+      for (int n = 0; n < 32; ++n)
+        for (int i = 0; i < 16; ++i) {
+          const float a = (float)n * fr.f[i];
+          c[n * 16 + i] = std::cos(a);
+          sn[n * 16 + i] = std::sin(a);
+        }
+      rope_cos = dmalloc(c.size() * 4);
+      rope_sin = dmalloc(sn.size() * 4);
+      HIPCHK(hipMemcpy(rope_cos, c.data(), c.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(rope_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
+    }
+    // window relative-position bias, dense per layer: bias[h][i][j] = table[index[i][j]][h]
+    for (auto& kv : host) {
+      const std::string& n = kv.first;
+      const std::string suf = ".fn.fn.attn.relative_position_bias_table";
+      if (n.size() <= suf.size() || n.compare(n.size() - suf.size(), suf.size(), suf) != 0) continue;
+      const std::string p = n.substr(0, n.size() - suf.size());
+      const HostTensor& tab = kv.second;
+      const HostTensor& idx = H(p + ".fn.fn.attn.relative_position_index");
+      const int N = (int)idx.shape[0], nh = (int)tab.shape[1];
+      REQUIRE(N <= 32, "window larger than 32 tokens");
+      std::vector<float> d((size_t)nh * 1024, 0.f);
+      for (int h = 0; h < nh; ++h)
+        for (int i = 0; i < N; ++i)
+          for (int j = 0; j < N; ++j) d[(size_t)h * 1024 + i * 32 + j] = tab.f[(size_t)idx.i[(size_t)i * N + j] * nh + h];
+      float* dd = dmalloc(d.size() * 4);
+      HIPCHK(hipMemcpy(dd, d.data(), d.size() * 4, hipMemcpyHostToDevice));
+      bias_dense[p] = dd;
+    }
+    // temporal T5 relative-position bias (RelativePositionBias, u12:42-79), max_distance 32
+    {
+      const HostTensor& emb = H("time_rel_pos_bias.relative_attention_bias.weight");
+      const int nh = (int)emb.shape[1], T = cfg.tc + cfg.tp;
+      REQUIRE(T <= 32, "temporal attention over more than 32 frames");
+      std::vector<float> d((size_t)nh * 1024, 0.f);
+      const int nb = 16, max_exact = 8;
+      for (int i = 0; i < T; ++i)
+        for (int j = 0; j < T; ++j) {
+          int n = -(j - i);
+          int ret = n < 0 ? nb : 0;
+          n = std::abs(n);
+          int bucket;
+          if (n < max_exact) {
+            bucket = ret + n;
+          } else {
+            const float v = std::log((float)n / (float)max_exact) / (float)std::log(32.0 / max_exact) *
+                            (float)(nb - max_exact);
+            int large = max_exact + (int)(int64_t)v;
+            large = std::min(large, nb - 1);
+            bucket = ret + large;
+          }
+          for (int h = 0; h < nh; ++h) d[(size_t)h * 1024 + i * 32 + j] = emb.f[(size_t)bucket * nh + h];
+        }
+      time_bias = dmalloc(d.size() * 4);
+      HIPCHK(hipMemcpy(time_bias, d.data(), d.size() * 4, hipMemcpyHostToDevice));
+    }
+    HIPCHK(hipDeviceSynchronize());
+  }
+
+  void finalize() {
+    REQUIRE(cfg.dim_head == 32, "this build supports attn_dim_head == 32");
+    REQUIRE(cfg.heads % 4 == 0, "attn_heads must be a multiple of 4");
+    HIPCHK(hipSetDevice(cfg.device));
+    s = 0;
+    // small tensors (biases, norm gains) go to the device now so that no
+    // host->device copy can happen while a sampler step is being captured
+    for (auto& kv : host)
+      if (!kv.second.is_int && kv.second.f.size() <= (1u << 16)) D(kv.first);
+    build_tables();
+    // pack every weight the forward touches by running it in planning mode
+    const int B = cfg.max_batch;
+    plan = true;
+    arena.planning = true;
+    arena.top = arena.peak = 0;
+    unet_forward(B, nullptr, nullptr, nullptr, nullptr);
+    plan = false;
+    arena.planning = false;
+    const size_t need = arena.peak + (1 << 20);
+    arena.base = reinterpret_cast<char*>(dmalloc(need));
+    arena.cap = need;
+    arena.top = 0;
+    const size_t n = (size_t)3 * cfg.tp * cfg.latent * cfg.latent;
+    eps_buf = dmalloc((size_t)B * n * sizeof(float));
+    partials = reinterpret_cast<double*>(dmalloc((size_t)B * 8 * 64 * 2 * sizeof(double)));
+    t_batch = reinterpret_cast<int*>(dmalloc((size_t)std::max(B, 1) * sizeof(int)));
+    step_ctr = reinterpret_cast<int*>(dmalloc(sizeof(int) * 4));
+    HIPCHK(hipStreamCreateWithFlags(&work, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
+    finalized = true;
+  }
+
+  void ensure_coefs(int S) {
+    if (S <= coefs_cap) return;
+    coefs = reinterpret_cast<StepCoef*>(dmalloc((size_t)S * sizeof(StepCoef)));
+    coefs_cap = S;
+  }
+
+  // Per-step coefficients in fp32 with the reference's expressions.
+  StepCoef make_coef(int sampler, int t, int t_next, float eta) {
+    StepCoef c{};
+    c.t = t;
+    c.sra = H("sqrt_recip_alphas_cumprod").f.at(t);
+    c.srm1 = H("sqrt_recipm1_alphas_cumprod").f.at(t);
+    if (sampler == EXTDM_SAMPLER_DDPM) {
+      c.kind = 0;
+      c.c1 = H("posterior_mean_coef1").f.at(t);
+      c.c2 = H("posterior_mean_coef2").f.at(t);
+      const float lv = H("posterior_log_variance_clipped").f.at(t);
+      const float nz = t == 0 ? 0.f : 1.f;  // Diffusion.py:176
+      volatile float half_lv = 0.5f * lv;
+      c.sigma = nz * std::exp((float)half_lv);
+      c.use_noise = 1;  // the reference draws noise even at t == 0 (multiplied by 0)
+    } else {
+      c.kind = 1;
+      // Diffusion.py:221-222 — alphas_cumprod_prev for both alpha and alpha_next
+      const float alpha = H("alphas_cumprod_prev").f.at(t);
+      const float an = H("alphas_cumprod_prev").f.at(t_next);
+      volatile float r1 = 1.f - alpha / an;
+      volatile float r2 = r1 * (1.f - an);
+      volatile float r3 = r2 / (1.f - alpha);
+      const float sigma = eta * std::sqrt((float)r3);
+      volatile float sig2 = sigma * sigma;
+      volatile float cc = (1.f - an) - (float)sig2;
+      c.sigma = sigma;
+      c.c1 = std::sqrt(an);
+      c.c2 = std::sqrt((float)cc);
+      c.use_noise = t_next > 0 ? 1 : 0;
+    }
+    return c;
+  }
+
+  void quantile_ranks(int n, int& klo, int& khi, float& w) const {
+    // torch.quantile: rank = q * (n - 1) in fp32, lerp between floor / ceil
+    volatile float q = 0.9f;
+    volatile float rank = q * (float)(n - 1);
+    klo = (int)(int64_t)rank;
+    khi = (int)(int64_t)std::ceil((float)rank);
+    w = (float)rank - (float)klo;
+  }
+};
+
+// ---------------------------------------------------------------- C ABI
+namespace {
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return -1;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+const char* extdm_last_error(void) { return g_last_error.c_str(); }
+
+int extdm_create(const ExtdmConfig* cfg, ExtdmHandle** out) {
+  return guarded([&] {
+    REQUIRE(cfg && out, "null argument");
+    REQUIRE(cfg->arch == EXTDM_ARCH_U12, "unsupported Unet3D architecture id");
+    REQUIRE(cfg->n_levels >= 1 && cfg->n_levels <= 4, "n_levels must be 1..4");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    REQUIRE(ndev > 0, "no HIP device visible");
+    auto h = std::make_unique<ExtdmHandle>();
+    h->cfg = *cfg;
+    HIPCHK(hipSetDevice(cfg->device));
+    *out = h.release();
+  });
+}
+
+void extdm_destroy(ExtdmHandle* h) {
+  if (!h) return;
+  hipSetDevice(h->cfg.device);
+  hipDeviceSynchronize();
+  if (h->work) hipStreamDestroy(h->work);
+  if (h->ev_in) hipEventDestroy(h->ev_in);
+  if (h->ev_out) hipEventDestroy(h->ev_out);
+  for (void* p : h->allocations) hipFree(p);
+  delete h;
+}
+
+int extdm_load_weight(ExtdmHandle* h, const char* name, const void* ptr, int dtype, const int64_t* shape, int ndim) {
+  return guarded([&] {
+    REQUIRE(h && name && ptr, "null argument");
+    REQUIRE(!h->finalized, "weights are frozen after extdm_finalize");
+    HostTensor t;
+    size_t n = 1;
+    for (int i = 0; i < ndim; ++i) { t.shape.push_back(shape[i]); n *= (size_t)shape[i]; }
+    if (dtype == 1) {
+      t.is_int = true;
+      t.i.assign(reinterpret_cast<const int64_t*>(ptr), reinterpret_cast<const int64_t*>(ptr) + n);
+    } else {
+      REQUIRE(dtype == 0, "dtype must be 0 (float32) or 1 (int64)");
+      t.f.assign(reinterpret_cast<const float*>(ptr), reinterpret_cast<const float*>(ptr) + n);
+    }
+    h->host[name] = std::move(t);
+  });
+}
+
+int extdm_finalize(ExtdmHandle* h) {
+  return guarded([&] {
+    REQUIRE(h, "null handle");
+    h->finalize();
+  });
+}
+
+int64_t extdm_workspace_bytes(const ExtdmHandle* h) { return h ? (int64_t)h->arena.cap : 0; }
+
+int extdm_unet_forward(ExtdmHandle* h, int B, const float* x, const int64_t* t, const float* cond, const float* fea,
+                       float* out, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && h->finalized, "handle not finalized");
+    REQUIRE(B >= 1 && B <= h->cfg.max_batch, "batch exceeds max_batch");
+    HIPCHK(hipSetDevice(h->cfg.device));
+    h->s = reinterpret_cast<hipStream_t>(stream);
+    t_to_int(h->s, t, h->t_batch, B);
+    h->unet_forward(B, x, cond, fea, out);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, float eta, float* x, const float* eps,
+                       const float* noise, float* thresh_out, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && h->finalized, "handle not finalized");
+    REQUIRE(B >= 1 && B <= h->cfg.max_batch, "batch exceeds max_batch");
+    HIPCHK(hipSetDevice(h->cfg.device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    h->ensure_coefs(1);
+    StepCoef c = h->make_coef(sampler, t, t_next, eta);
+    HIPCHK(hipMemcpyAsync(h->coefs, &c, sizeof(c), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(h->step_ctr, 0, sizeof(int), s));
+    const int n = 3 * h->cfg.tp * h->cfg.latent * h->cfg.latent;
+    int klo, khi;
+    float w;
+    h->quantile_ranks(n, klo, khi, w);
+    sampler_step(s, x, eps, B, n, h->coefs, h->step_ctr, noise, 0, 0, 0, klo, khi, w, thresh_out);
+    HIPCHK(hipStreamSynchronize(s));  // `c` is a host temporary
+  });
+}
+
+int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, const int* times_next, float eta,
+                 const float* x_cond, const float* cond_fea, const float* x_T, const float* noise, uint64_t seed,
+                 int sample_base, int round, float* out, int use_graph, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && h->finalized, "handle not finalized");
+    REQUIRE(B >= 1 && B <= h->cfg.max_batch, "batch exceeds max_batch");
+    REQUIRE(S >= 1 && times, "empty schedule");
+    HIPCHK(hipSetDevice(h->cfg.device));
+    hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
+    hipStream_t s = h->work;
+    h->s = s;
+    HIPCHK(hipEventRecord(h->ev_in, caller));
+    HIPCHK(hipStreamWaitEvent(s, h->ev_in, 0));
+    h->ensure_coefs(S);
+    std::vector<StepCoef> cs(S);
+    for (int k = 0; k < S; ++k) cs[k] = h->make_coef(sampler, times[k], times_next ? times_next[k] : 0, eta);
+    HIPCHK(hipMemcpyAsync(h->coefs, cs.data(), S * sizeof(StepCoef), hipMemcpyHostToDevice, s));
+    const int n = 3 * h->cfg.tp * h->cfg.latent * h->cfg.latent;
+    if (x_T) HIPCHK(hipMemcpyAsync(out, x_T, (size_t)B * n * sizeof(float), hipMemcpyDeviceToDevice, s));
+    else fill_normal(s, out, B, n, seed, sample_base, round, 0x7FFFFFFF);
+    HIPCHK(hipMemsetAsync(h->step_ctr, 0, sizeof(int), s));
+    int klo, khi;
+    float w;
+    h->quantile_ranks(n, klo, khi, w);
+    auto step = [&]() {
+      set_t_from_step(s, h->t_batch, B, h->coefs, h->step_ctr);
+      h->unet_forward(B, out, x_cond, cond_fea, h->eps_buf);
+      sampler_step(s, out, h->eps_buf, B, n, h->coefs, h->step_ctr, noise, seed, sample_base, round, klo, khi, w,
+                   nullptr);
+      incr_counter(s, h->step_ctr);
+    };
+    if (use_graph) {
+      hipGraph_t graph;
+      hipGraphExec_t exec;
+      HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+      step();
+      HIPCHK(hipStreamEndCapture(s, &graph));
+      HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      for (int k = 0; k < S; ++k) HIPCHK(hipGraphLaunch(exec, s));
+      HIPCHK(hipStreamSynchronize(s));  // the host coefficient vector must outlive the copies
+      HIPCHK(hipGraphExecDestroy(exec));
+      HIPCHK(hipGraphDestroy(graph));
+    } else {
+      for (int k = 0; k < S; ++k) step();
+      HIPCHK(hipStreamSynchronize(s));
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(h->ev_out, s));
+    HIPCHK(hipStreamWaitEvent(caller, h->ev_out, 0));
+  });
+}
+
+int extdm_decode(ExtdmHandle* h, int B, int C, int T, int S, int fh, int fw, const float* ref, const float* flow,
+                 float* out, void* stream) {
+  return guarded([&] {
+    REQUIRE(h, "null handle");
+    HIPCHK(hipSetDevice(h->cfg.device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    warp_frames(s, out, ref, flow, B, C, T, S, fh, fw, (long)C * T * S * S, (long)T * S * S, (long)S * S);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+}  // extern "C"

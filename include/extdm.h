@@ -1,0 +1,97 @@
+/* ExtDM sampling path — C ABI of libextdm_hip.so (MI355X / gfx950).
+ *
+ * The drop-in boundary under the package's Python mirror of the reference API.
+ * Plain pointers and sizes only; every tensor is fp32, contiguous NCDHW
+ * (`b c t h w`) and caller-owned; device pointers live on the handle's device.
+ * Every function returns 0 on success or a negative status; the message is in
+ * extdm_last_error() (thread-local), which the Python layer raises as
+ * RuntimeError. A handle is not thread-safe; different handles may run
+ * concurrently (one per device / process).
+ *
+ * Reference interfaces replaced (file:line in the reference tree):
+ *   extdm_create / extdm_load_weight / extdm_finalize
+ *       Unet3D.__init__ + load_state_dict          DenoiseNet_..._u12.py:864-1003
+ *       GaussianDiffusion.__init__ buffers          Diffusion.py:52-122
+ *       Generator.__init__ (decoder half)           LFAE/generator.py:26-62
+ *   extdm_unet_forward   Unet3D.forward / forward_with_cond_scale(cond_scale=1)
+ *                                                   u12:1005-1086
+ *   extdm_sample         GaussianDiffusion.p_sample_loop / ddim_sample
+ *                                                   Diffusion.py:180-189, 209-258
+ *   extdm_sampler_step   one p_sample / DDIM update given eps
+ *                                                   Diffusion.py:145-177, 231-255
+ *   extdm_decode         Generator.forward_with_flow (occlusion_map=None path)
+ *                                                   LFAE/generator.py:152-206
+ */
+#ifndef EXTDM_H
+#define EXTDM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ExtdmHandle ExtdmHandle;
+
+enum { EXTDM_ARCH_U12 = 0 };
+enum { EXTDM_SAMPLER_DDPM = 0, EXTDM_SAMPLER_DDIM = 1 };
+
+typedef struct ExtdmConfig {
+  int arch;            /* EXTDM_ARCH_* (u12 == u22) */
+  int dim;             /* Unet base width (64) */
+  int channels;        /* init_conv input channels (256 + 256) */
+  int dim_mults[4];
+  int n_levels;        /* entries used in dim_mults */
+  int window[3];       /* (2, 4, 4) */
+  int heads;           /* attn_heads (8) */
+  int dim_head;        /* attn_dim_head (32) */
+  int tc, tp;          /* cond / pred frames */
+  int latent;          /* flow-latent H = W (32) */
+  int fea_size;        /* cond_fea H = W (16) */
+  int fea_ch;          /* cond_fea channels (256) */
+  int timesteps;       /* diffusion T (1000) */
+  int max_batch;       /* workspace is sized for this batch */
+  int device;          /* HIP device ordinal */
+} ExtdmConfig;
+
+int extdm_create(const ExtdmConfig* cfg, ExtdmHandle** out);
+void extdm_destroy(ExtdmHandle* h);
+const char* extdm_last_error(void);
+
+/* Copy one named tensor (reference state_dict key: Unet keys without the
+ * `denoise_fn.` prefix, GaussianDiffusion buffers by their own names, decoder
+ * keys with a `generator.` prefix). dtype: 0 = float32, 1 = int64. Host memory. */
+int extdm_load_weight(ExtdmHandle* h, const char* name, const void* host_ptr, int dtype, const int64_t* shape,
+                      int ndim);
+/* Pack weights into the GEMM layouts, build t-only tables (time-MLP, FiLM,
+ * rotary, relative-position biases) and the workspace. */
+int extdm_finalize(ExtdmHandle* h);
+int64_t extdm_workspace_bytes(const ExtdmHandle* h);
+
+/* eps = Unet3D(x, t, cond_frames, cond_fea). x, out: [B,3,tp,L,L]; t: int64 [B];
+ * cond: [B,3,tc,L,L]; fea: [B,fea_ch,tc+tp,fs,fs]. All device pointers. */
+int extdm_unet_forward(ExtdmHandle* h, int B, const float* x, const int64_t* t, const float* cond,
+                       const float* fea, float* out, void* stream);
+
+/* Whole reverse loop. times[k] is the model timestep of step k and
+ * times_next[k] the DDIM target (ignored for DDPM). x_T (device, may be NULL:
+ * Philox stream), noise (device [S][B][n] or NULL: Philox stream), out (device
+ * [B,3,tp,L,L]) receives x_0. use_graph != 0 replays one captured step. */
+int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, const int* times_next, float eta,
+                 const float* x_cond, const float* cond_fea, const float* x_T, const float* noise, uint64_t seed,
+                 int sample_base, int round, float* out, int use_graph, void* stream);
+
+/* One sampler update in place on x given eps (the step-k coefficients). */
+int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, float eta, float* x, const float* eps,
+                       const float* noise, float* thresh_out, void* stream);
+
+/* LFAE decoder for occlusion_map=None: prediction (== deformed) of every frame.
+ * ref: [B,C,S,S]; flow: [B,2,T,fh,fw] (x, y); out: [B,C,T,S,S]. */
+int extdm_decode(ExtdmHandle* h, int B, int C, int T, int S, int fh, int fw, const float* ref, const float* flow,
+                 float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EXTDM_H */

@@ -1,0 +1,202 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference golden
+vectors and the CPU oracle on the same seeded inputs.
+
+Tolerances (fp32 everywhere; the reference's own fp32-vs-fp64 drift is 2.5e-6
+per eps forward):
+  eps (Unet3D output, |eps| ~ 2)    max-abs <= 1e-4
+  one DDPM / DDIM update            max-abs <= 1e-5 x (1 + |eps| coefficient)
+  quantile threshold                bit-exact
+  DDPM step indexing / DDIM pairs   exact
+"""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_inputs import CONFIGS, PKG, make_sd, unet_inputs, make_gen_sd, decoder_inputs, GEN_CFG
+from tests.test_oracle_golden import load
+
+pytestmark = pytest.mark.gpu
+
+pkg = importlib.import_module(PKG)
+DEV = torch.device('cuda:0')
+_HANDLES = {}
+
+
+def handle(name, max_batch=4):
+    key = (name, max_batch)
+    if key not in _HANDLES:
+        cfg = CONFIGS[name]
+        h = pkg._lib.Handle(cfg, 1000, max_batch, 0)
+        sd = make_sd(cfg)
+        sd.update(pkg.schedule_buffers(1000))
+        h.load_state(sd)
+        h.finalize()
+        _HANDLES[key] = h
+    return _HANDLES[key]
+
+
+def oracle():
+    from oracle import extdm_oracle as O
+    return O
+
+
+def gpu_eps(h, x, t, cond, fea):
+    out = torch.empty(x.shape, device=DEV)
+    h.unet_forward(x.to(DEV), t.to(DEV), cond.to(DEV), fea.to(DEV), out)
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+@pytest.mark.parametrize('name', ['small', 'bair'])
+def test_unet_forward_vs_reference_golden(name):
+    cfg = CONFIGS[name]
+    x, t, cond, fea = unet_inputs(cfg)
+    eps = gpu_eps(handle(name), x, t, cond, fea)
+    g = load(f'unet_{name}.npz')['eps']
+    err = np.abs(eps.numpy() - g).max()
+    assert err <= 1e-4, err
+
+
+def test_unet_forward_vs_oracle_other_t():
+    cfg = CONFIGS['small']
+    x, _, cond, fea = unet_inputs(cfg, B=3, seed=7)
+    t = torch.tensor([0, 250, 998])
+    eps = gpu_eps(handle('small'), x, t, cond, fea)
+    with torch.no_grad():
+        ref = oracle().unet_forward(make_sd(cfg), cfg.as_dict(), x, t, cond, fea)
+    assert (eps - ref).abs().max().item() <= 1e-4
+
+
+def test_batch_independence_bitwise():
+    """Per-sample results do not depend on batch composition (sharding-safe)."""
+    cfg = CONFIGS['small']
+    x, t, cond, fea = unet_inputs(cfg, B=4, seed=3)
+    t = torch.tensor([10, 20, 30, 40])
+    h = handle('small')
+    full = gpu_eps(h, x, t, cond, fea)
+    one = gpu_eps(h, x[2:3].contiguous(), t[2:3], cond[2:3].contiguous(), fea[2:3].contiguous())
+    assert torch.equal(full[2:3], one)
+
+
+def test_ddpm_steps_vs_reference_golden():
+    cfg = CONFIGS['small']
+    x, _, cond, fea = unet_inputs(cfg)
+    g = load('sampler_small.npz')
+    h = handle('small')
+    for ti in (999, 500, 1, 0):
+        tt = torch.full((2,), ti, dtype=torch.long)
+        eps = gpu_eps(h, x, tt, cond, fea).to(DEV)
+        torch.manual_seed(100 + ti)
+        noise = torch.randn(x.shape)
+        xs = x.to(DEV).contiguous()
+        h.sampler_step(0, ti, 0, 0., xs, eps, noise.to(DEV)[None].contiguous())
+        torch.cuda.synchronize()
+        err = np.abs(xs.cpu().numpy() - g[f'p_sample_{ti}']).max()
+        assert err <= 1e-4, (ti, err)
+
+
+def test_quantile_threshold_bit_exact():
+    """The fused step's radix-select threshold equals torch.quantile bit for bit."""
+    cfg = CONFIGS['small']
+    h = handle('small')
+    sch = pkg.schedule_buffers(1000)
+    gen = torch.Generator().manual_seed(1)
+    n = 3 * cfg.tp * cfg.latent * cfg.latent
+    for ti, scale in ((999, 1.0), (500, 3.0), (3, 0.2), (100, 50.0)):
+        x = (torch.randn(3, 3, cfg.tp, cfg.latent, cfg.latent, generator=gen) * scale)
+        eps = torch.randn(x.shape, generator=gen)
+        x[1].view(-1)[: n // 2] = 0.25  # heavy ties
+        x0 = sch['sqrt_recip_alphas_cumprod'][ti] * x - sch['sqrt_recipm1_alphas_cumprod'][ti] * eps
+        ref = torch.quantile(x0.reshape(3, -1).abs(), 0.9, dim=-1).clamp(min=1.0)
+        th = torch.zeros(3, device=DEV)
+        xs = x.to(DEV).contiguous()
+        h.sampler_step(0, ti, 0, 0., xs, eps.to(DEV).contiguous(), torch.zeros((1,) + x.shape, device=DEV), th)
+        torch.cuda.synchronize()
+        assert torch.equal(th.cpu(), ref), (ti, th.cpu(), ref)
+
+
+@pytest.mark.parametrize('use_graph', [True, False])
+def test_ddpm10_chain_vs_reference_golden(use_graph):
+    cfg = CONFIGS['small']
+    x, _, cond, fea = unet_inputs(cfg)
+    g = load('sampler_small.npz')
+    h10 = pkg._lib.Handle(cfg, 10, 2, 0)
+    sd = make_sd(cfg)
+    sd.update(pkg.schedule_buffers(10))
+    h10.load_state(sd)
+    h10.finalize()
+    torch.manual_seed(7)
+    xT = torch.randn(x.shape)
+    noises = torch.stack([torch.randn(x.shape) for _ in range(10)])
+    out = torch.empty(x.shape, device=DEV)
+    h10.sample(0, list(range(9, -1, -1)), None, 0., cond.to(DEV), fea.to(DEV), out, x_T=xT.to(DEV),
+               noise=noises.to(DEV).contiguous(), use_graph=use_graph)
+    torch.cuda.synchronize()
+    err = np.abs(out.cpu().numpy() - g['ddpm10']).max()
+    assert err <= 2e-4, err
+
+
+def test_ddim10_chain_vs_reference_golden():
+    cfg = CONFIGS['small']
+    x, _, cond, fea = unet_inputs(cfg)
+    g = load('sampler_small.npz')
+    h = handle('small')
+    pairs = pkg.ddim_time_pairs(1000, 10)
+    torch.manual_seed(11)
+    xT = torch.randn(x.shape)
+    noises = torch.stack([torch.randn(x.shape) for _ in range(10)])
+    out = torch.empty(x.shape, device=DEV)
+    h.sample(1, [p[0] for p in pairs], [p[1] for p in pairs], 1.0, cond.to(DEV), fea.to(DEV), out, x_T=xT.to(DEV),
+             noise=noises.to(DEV).contiguous())
+    torch.cuda.synchronize()
+    err = np.abs(out.cpu().numpy() - g['ddim10']).max()
+    assert err <= 2e-4, err
+
+
+def test_graph_equals_eager_and_sharding_invariance():
+    """Philox noise keyed by global sample index: a 4-sample batch equals two
+    2-sample shards with sample_base 0 and 2, bit for bit; graph == eager."""
+    cfg = CONFIGS['small']
+    x, _, cond, fea = unet_inputs(cfg, B=4, seed=21)
+    h = handle('small')
+    times = list(range(999, 989, -1))
+    outs = {}
+    for use_graph in (True, False):
+        o = torch.empty(x.shape, device=DEV)
+        h.sample(0, times, None, 0., cond.to(DEV), fea.to(DEV), o, seed=1234, sample_base=0, use_graph=use_graph)
+        outs[use_graph] = o.cpu()
+    assert torch.equal(outs[True], outs[False])
+    parts = []
+    for base in (0, 2):
+        o = torch.empty((2,) + tuple(x.shape[1:]), device=DEV)
+        h.sample(0, times, None, 0., cond[base:base + 2].to(DEV).contiguous(), fea[base:base + 2].to(DEV).contiguous(),
+                 o, seed=1234, sample_base=base)
+        parts.append(o.cpu())
+    assert torch.equal(torch.cat(parts), outs[True])
+
+
+def test_decoder_no_occlusion_vs_reference_golden():
+    src, flow, _ = decoder_inputs()
+    g = load('decoder.npz')
+    gen = pkg.Generator()
+    out = gen.forward_with_flow(src.to(DEV), flow.to(DEV), None)
+    err = np.abs(out['prediction'].cpu().numpy() - g['pred_noocc']).max()
+    assert err <= 1e-5, err
+    assert torch.equal(out['prediction'], out['deformed'])
+
+
+def test_drop_in_api_sample_shapes_and_determinism():
+    cfg = CONFIGS['small']
+    u = pkg.Unet3D(dim=cfg.dim, channels=512, dim_mults=cfg.dim_mults, cond_num=cfg.tc, pred_num=cfg.tp,
+                   framesize=cfg.latent).to(DEV)
+    d = pkg.GaussianDiffusion(u, image_size=cfg.latent, num_frames=cfg.tc + cfg.tp, timesteps=1000,
+                              sampling_timesteps=10).to(DEV)
+    x, _, cond, fea = unet_inputs(cfg)
+    torch.manual_seed(5)
+    a = d.sample(cond.to(DEV), cond_fea=fea.to(DEV))
+    torch.manual_seed(5)
+    b = d.sample(cond.to(DEV), cond_fea=fea.to(DEV))
+    assert a.shape == (2, 3, cfg.tp, cfg.latent, cfg.latent)
+    assert torch.equal(a, b) and torch.isfinite(a).all()
