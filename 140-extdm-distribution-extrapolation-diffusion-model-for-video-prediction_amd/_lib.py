@@ -9,7 +9,8 @@ LIB_PATH = os.path.join(HERE, 'libextdm_hip.so')
 
 # every symbol include/extdm.h declares
 EXPORTS = ['extdm_create', 'extdm_destroy', 'extdm_last_error', 'extdm_load_weight', 'extdm_finalize',
-           'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_decode']
+           'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_bench_layer',
+           'extdm_decode']
 
 SAMPLER_DDPM = 0
 SAMPLER_DDIM = 1
@@ -54,6 +55,8 @@ def load():
     L.extdm_sample.restype = i32
     L.extdm_sampler_step.argtypes = [vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp]
     L.extdm_sampler_step.restype = i32
+    L.extdm_bench_layer.argtypes = [vp, i32, i32, i32, ctypes.POINTER(f32), ctypes.POINTER(ctypes.c_double)]
+    L.extdm_bench_layer.restype = i32
     L.extdm_decode.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]
     L.extdm_decode.restype = i32
     _lib = L
@@ -160,6 +163,11 @@ class Handle:
         _require_device(x, eps, noise, thresh_out)
         check(load().extdm_sampler_step(self.h, x.shape[0], sampler, int(t), int(t_next), float(eta), _ptr(x),
                                         _ptr(eps), _ptr(noise), _ptr(thresh_out), _stream()))
+
+    def bench_layer(self, B, layer=0, iters=20):
+        ms, fl = ctypes.c_float(), ctypes.c_double()
+        check(load().extdm_bench_layer(self.h, B, layer, iters, ctypes.byref(ms), ctypes.byref(fl)))
+        return float(ms.value), float(fl.value)
 
     def decode(self, ref, flow, out):
         _require_device(ref, flow, out)

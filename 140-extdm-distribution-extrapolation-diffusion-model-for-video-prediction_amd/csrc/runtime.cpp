@@ -701,12 +701,12 @@ int extdm_create(const ExtdmConfig* cfg, ExtdmHandle** out) {
 
 void extdm_destroy(ExtdmHandle* h) {
   if (!h) return;
-  hipSetDevice(h->cfg.device);
-  hipDeviceSynchronize();
-  if (h->work) hipStreamDestroy(h->work);
-  if (h->ev_in) hipEventDestroy(h->ev_in);
-  if (h->ev_out) hipEventDestroy(h->ev_out);
-  for (void* p : h->allocations) hipFree(p);
+  (void)hipSetDevice(h->cfg.device);
+  (void)hipDeviceSynchronize();
+  if (h->work) (void)hipStreamDestroy(h->work);
+  if (h->ev_in) (void)hipEventDestroy(h->ev_in);
+  if (h->ev_out) (void)hipEventDestroy(h->ev_out);
+  for (void* p : h->allocations) (void)hipFree(p);
   delete h;
 }
 
@@ -819,6 +819,40 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(h->ev_out, s));
     HIPCHK(hipStreamWaitEvent(caller, h->ev_out, 0));
+  });
+}
+
+int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out, double* flops_out) {
+  return guarded([&] {
+    REQUIRE(h && h->finalized, "handle not finalized");
+    REQUIRE(B >= 1 && B <= h->cfg.max_batch, "batch exceeds max_batch");
+    HIPCHK(hipSetDevice(h->cfg.device));
+    hipStream_t s = h->work;
+    h->s = s;
+    Scope sc(h->arena);
+    const int T = h->cfg.tc + h->cfg.tp, L = h->cfg.latent;
+    // layer 0: init_conv, conv3d (1,7,7) 512 -> dim over (B, T, L, L) (u12:913, 1041)
+    REQUIRE(layer == 0, "unknown layer id");
+    View x0 = h->alloc_cf(B, 256, T, L, L), fup = h->alloc_cf(B, h->cfg.channels - 256, T, L, L);
+    View r = h->alloc_cf(B, h->cfg.dim, T, L, L);
+    HIPCHK(hipMemsetAsync(x0.p, 0, x0.numel() * 4, s));
+    HIPCHK(hipMemsetAsync(fup.p, 0, fup.numel() * 4, s));
+    const PackedW& w = h->P("init_conv.weight");
+    float* bias = h->D("init_conv.bias");
+    h->conv(r, x0, &fup, w, 1, 3, bias);  // warm
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, s));
+    for (int i = 0; i < iters; ++i) h->conv(r, x0, &fup, w, 1, 3, bias);
+    HIPCHK(hipEventRecord(b, s));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *ms_out = ms / iters;
+    *flops_out = 2.0 * B * T * L * L * (double)h->cfg.dim * h->cfg.channels * 49.0;
   });
 }
 

@@ -85,6 +85,12 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
 int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, float eta, float* x, const float* eps,
                        const float* noise, float* thresh_out, void* stream);
 
+/* Measurement hook for bench.py: time `iters` launches of one hot-path kernel
+ * exactly as the forward issues it (layer 0 = init_conv, the (1,7,7) 512->dim
+ * conv) with HIP events on the handle's stream; returns the average ms per
+ * launch and the algorithmic FLOPs per launch. */
+int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out, double* flops_out);
+
 /* LFAE decoder for occlusion_map=None: prediction (== deformed) of every frame.
  * ref: [B,C,S,S]; flow: [B,2,T,fh,fw] (x, y); out: [B,C,T,S,S]. */
 int extdm_decode(ExtdmHandle* h, int B, int C, int T, int S, int fh, int fw, const float* ref, const float* flow,
