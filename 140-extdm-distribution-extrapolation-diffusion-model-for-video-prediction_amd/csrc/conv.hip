@@ -11,6 +11,8 @@
 // fmaf chain), so numerics are those of an fp32 conv.
 // MODE_DECONV runs ConvTranspose(1,4,4)/s2/p1 as four 2x2 parity convs
 // (blockIdx.z = parity); MODE_UP2 reads a nearest-x2-upsampled input.
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace extdm {
@@ -205,6 +207,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   }
 }
 
+bool getenv_flag(const char* n) {
+  static int cached = -1;
+  if (cached < 0) { const char* v = getenv(n); cached = (v && v[0] && v[0] != '0') ? 1 : 0; }
+  return cached == 1;
+}
+
 template <int KH, int KW, int MODE>
 void launch_bm(hipStream_t s, const ConvArgs& a, int bm, dim3 grid_n) {
   dim3 block(256);
@@ -224,6 +232,9 @@ void launch_bm(hipStream_t s, const ConvArgs& a, int bm, dim3 grid_n) {
 
 void conv_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                   int stride, int pad, const ConvEpi& epi) {
+  if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 && !getenv_flag("EXTDM_NO_HALO") &&
+      conv_halo_forward(s, out, in0, in1, w, epi))
+    return;
   ConvArgs a{};
   a.in0 = in0.p; a.i0b = in0.sb; a.i0c = in0.sc; a.i0t = in0.st;
   a.C0 = in0.C;

@@ -42,6 +42,9 @@ enum ConvMode { MODE_CONV = 0, MODE_DECONV = 1, MODE_UP2 = 2 };
 struct PackedW {
   float* w = nullptr;
   int K = 0, M = 0, Kpad = 0, Mpad = 0, KH = 1, KW = 1, mode = MODE_CONV;
+  // direct-conv (halo tile) layout [mtile][stage][step][half][BM], see conv_halo.hip
+  float* wh = nullptr;
+  int hstages = 0, hbm = 0;
 };
 
 // Output-channel tile of the conv GEMM for M output channels (Mpad is a multiple of it).
@@ -55,6 +58,12 @@ struct ConvEpi {
   const float* post_shift = nullptr;
   int act = ACT_NONE;
 };
+
+// Input channels per half-stage of the halo conv for kernel size ks and tile bm.
+int halo_ch(int ks, int bm);
+// Direct stride-1 'same' conv through LDS halo tiles; false if the geometry is not covered.
+bool conv_halo_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
+                       const ConvEpi& epi);
 
 // out = act(conv(in0 ++ in1) + bias + res) [* s + sh]
 void conv_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,

@@ -155,7 +155,34 @@ struct ExtdmHandle {
       for (int k = 0; k < pw.K; ++k) a[(size_t)k * pw.Mpad + m] = t.f[(size_t)m * pw.K + k];
     pw.w = dmalloc(a.size() * sizeof(float));
     HIPCHK(hipMemcpy(pw.w, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (kh == kw && (kh == 1 || kh == 3 || kh == 7) && co > 32) pack_halo(pw, t.f, ci);
     return packed[n] = pw;
+  }
+  // Direct-conv layout [mtile][stage][step][half][BM]: step = (cp*k + ky)*k + kx,
+  // input channel = stage*2CH + half*CH + cp (conv_halo.hip).
+  void pack_halo(PackedW& pw, const std::vector<float>& w, int ci) {
+    const int ks = pw.KH, kk = ks * ks, co = pw.M;
+    const int bm = conv_bm(co);
+    const int ch = halo_ch(ks, bm), cib = 2 * ch;
+    const int stages = (ci + cib - 1) / cib;
+    const int mt = (co + bm - 1) / bm;
+    const size_t afl = (size_t)ch * kk * 2 * bm;
+    std::vector<float> a((size_t)mt * stages * afl, 0.f);
+    for (int m = 0; m < co; ++m) {
+      const int mtile = m / bm, mm = m % bm;
+      for (int c = 0; c < ci; ++c) {
+        const int st = c / cib, rem = c % cib, half = rem / ch, cp = rem % ch;
+        for (int tap = 0; tap < kk; ++tap) {
+          const int step = cp * kk + tap;
+          a[((size_t)mtile * stages + st) * afl + ((size_t)step * 2 + half) * bm + mm] =
+              w[((size_t)m * ci + c) * kk + tap];
+        }
+      }
+    }
+    pw.wh = dmalloc(a.size() * sizeof(float));
+    HIPCHK(hipMemcpy(pw.wh, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
+    pw.hstages = stages;
+    pw.hbm = bm;
   }
   // ConvTranspose3d(1,4,4)/s2/p1 weight W[ci][co][1][4][4] -> four 2x2 parity GEMMs:
   // parity (py,px) tap (ky',kx') uses W[..][3-py-2ky'][3-px-2kx'].

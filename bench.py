@@ -38,7 +38,7 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=1)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--batch', type=int, default=16, help='clips per GPU')
+    ap.add_argument('--batch', type=int, default=32, help='clips per GPU')
     ap.add_argument('--sampling-steps', type=int, default=1000)
     ap.add_argument('--rounds', type=int, default=2)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -170,7 +170,8 @@ def main():
             'config': {'workload': f'BAIR 64x64 ch3 2->{args.rounds * tp} (tc={tc}, tp={tp} x {args.rounds} rounds), '
                                    f'DDPM {S} steps, u12 Unet3D dim 64 mults (1,2,4,4)',
                        'global_batch': world * B, 'batch_per_gpu': B, 'sampling_steps': S,
-                       'rounds': args.rounds, 'parallelism': f'clip-shard x{world} (+RCCL all-gather)'},
+                       'rounds': args.rounds, 'parallelism': f'clip-shard x{world} (+RCCL all-gather)',
+                       'workspace_gb': round(h.workspace_bytes() / 2 ** 30, 2)},
             'roofline': {'bound': 'mfma', 'kernel': 'conv_gemm_kernel<7,7,64> (init_conv 512->64, 1x7x7)',
                          'achieved': round(achieved, 2), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic},
