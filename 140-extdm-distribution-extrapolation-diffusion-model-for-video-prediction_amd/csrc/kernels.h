@@ -93,6 +93,11 @@ struct AttnGeom {
 void window_attention(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads,
                       const float* bias_dense /*[heads][32][32]*/, const float* rope_cos,
                       const float* rope_sin /*[32][16]*/, float q_scale);
+// Fused Residual(PreNorm(STWAttentionLayer)) in place on x (stw_fused.hip); false if
+// C not in {64,128,256} or heads != 8. Weights pre-packed (see the kernel header).
+bool stw_fused(hipStream_t s, const View& x, const AttnGeom& g, int heads, const float* gamma, const float* wqkv,
+               const float* wp, const float* bp, const float* bias_dense, const float* rcos, const float* rsin,
+               float q_scale);
 // TrajWarp cross-attention (u12:719-773): q [B][256][NQ], k,v [B][256][NK].
 void cross_attention(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,
                      int heads, int NQ, int NK);

@@ -296,8 +296,55 @@ struct ExtdmHandle {
     return g;
   }
 
+  // Packed weights of the fused STW kernel (stw_fused.hip header).
+  float* packed_stw_qkv(const std::string& n) {
+    auto it = dev.find(n + "#stwqkv");
+    if (it != dev.end()) return it->second;
+    const HostTensor& t = H(n);
+    const int C = (int)t.shape[1], heads = cfg.heads;
+    std::vector<float> a((size_t)heads * (C / 2) * 3 * 64);
+    for (int hd = 0; hd < heads; ++hd)
+      for (int s2 = 0; s2 < C / 2; ++s2)
+        for (int wh = 0; wh < 3; ++wh)
+          for (int l = 0; l < 64; ++l)
+            a[(((size_t)hd * (C / 2) + s2) * 3 + wh) * 64 + l] =
+                t.f[(size_t)(wh * heads * 32 + hd * 32 + (l & 31)) * C + 2 * s2 + (l >> 5)];
+    float* d = dmalloc(a.size() * 4);
+    HIPCHK(hipMemcpy(d, a.data(), a.size() * 4, hipMemcpyHostToDevice));
+    return dev[n + "#stwqkv"] = d;
+  }
+  float* packed_stw_proj(const std::string& n) {
+    auto it = dev.find(n + "#stwproj");
+    if (it != dev.end()) return it->second;
+    const HostTensor& t = H(n);
+    const int C = (int)t.shape[0], K = (int)t.shape[1];
+    std::vector<float> a((size_t)(C / 32) * (K / 2) * 64);
+    for (int tl = 0; tl < C / 32; ++tl)
+      for (int s2 = 0; s2 < K / 2; ++s2)
+        for (int l = 0; l < 64; ++l)
+          a[((size_t)tl * (K / 2) + s2) * 64 + l] = t.f[(size_t)(tl * 32 + (l & 31)) * K + 2 * s2 + (l >> 5)];
+    float* d = dmalloc(a.size() * 4);
+    HIPCHK(hipMemcpy(d, a.data(), a.size() * 4, hipMemcpyHostToDevice));
+    return dev[n + "#stwproj"] = d;
+  }
+  bool fused_stw_ok(int C) const {
+    static const bool off = [] { const char* v = getenv("EXTDM_NO_FUSED_STW"); return v && v[0] && v[0] != '0'; }();
+    return !off && cfg.heads == 8 && cfg.dim_head == 32 && (C == 64 || C == 128 || C == 256);
+  }
+
   // Residual(PreNorm(STWAttentionLayer)) in place on x (u12:498-559, 961-963)
   void stw(const std::string& p, const View& x, bool shifted) {
+    if (fused_stw_ok(x.C)) {
+      const std::string a = p + ".fn.fn.attn";
+      float* wq = packed_stw_qkv(a + ".qkv.weight");
+      float* wp = packed_stw_proj(a + ".proj.weight");
+      if (plan) return;
+      const AttnGeom g = stw_geom(x.T, x.H, x.W, shifted);
+      REQUIRE(stw_fused(s, x, g, cfg.heads, D(p + ".fn.norm.gamma"), wq, wp, D(a + ".proj.bias"), bias_dense.at(p),
+                        rope_cos, rope_sin, 1.0f / std::sqrt((float)cfg.dim_head)),
+              "fused STW launch rejected");
+      return;
+    }
     Scope sc(arena);
     const int hid = cfg.heads * 32;
     View ln = alloc_cf(x.B, x.C, x.T, x.H, x.W);

@@ -172,7 +172,7 @@ def main():
                        'global_batch': world * B, 'batch_per_gpu': B, 'sampling_steps': S,
                        'rounds': args.rounds, 'parallelism': f'clip-shard x{world} (+RCCL all-gather)',
                        'workspace_gb': round(h.workspace_bytes() / 2 ** 30, 2)},
-            'roofline': {'bound': 'mfma', 'kernel': 'conv_gemm_kernel<7,7,64> (init_conv 512->64, 1x7x7)',
+            'roofline': {'bound': 'mfma', 'kernel': 'conv_halo_kernel<7,64,1> (init_conv 512->64, 1x7x7)',
                          'achieved': round(achieved, 2), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic},
         }
