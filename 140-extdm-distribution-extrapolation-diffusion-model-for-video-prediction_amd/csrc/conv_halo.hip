@@ -49,7 +49,7 @@ template <> struct XMax<1> { static constexpr int v = 128; };
 template <> struct XMax<3> { static constexpr int v = 288; };
 template <> struct XMax<7> { static constexpr int v = 560; };
 
-template <int KS, int BM, int CH>
+template <int KS, int BM, int CH, int BNP>
 __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a) {
   constexpr int KK = KS * KS;
   constexpr int PAD = KS / 2;
@@ -57,10 +57,12 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a) {
   constexpr int STEPS = CH * KK;
   constexpr int AFL = STEPS * 2 * BM;          // A floats per stage
   constexpr int XJ = (CIB * XMax<KS>::v + 255) / 256;
-  constexpr int WAVES_M = BM >= 64 ? 2 : 1;
-  constexpr int WAVES_N = 4 / WAVES_M;
+  // BNP = pixels per block tile: 128 (2x2 waves) or 32 (4 waves stacked over BM = 128)
+  constexpr int WAVES_N = BNP == 128 ? (BM >= 64 ? 2 : 4) : 1;
+  constexpr int WAVES_M = 4 / WAVES_N;
   constexpr int TM = BM / (32 * WAVES_M);
-  constexpr int TN = 128 / (32 * WAVES_N);
+  constexpr int TN = BNP / (32 * WAVES_N);
+  static_assert(TM >= 1 && TN >= 1, "bad tile");
 
   extern __shared__ float smem[];
   const int XFL = CIB * a.XPC;
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a) {
   int boff[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int n = (wn * TN + j) * 32 + lc;
+    const int n = (wn * TN + j) * 32 + lc;  // pixel within the block tile
     const int p = n / (a.TH * a.W);
     const int r = (n / a.W) % a.TH;
     const int c = n % a.W;
@@ -217,18 +219,18 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a) {
   }
 }
 
-template <int KS, int BM, int CH>
+template <int KS, int BM, int CH, int BNP>
 void launch(hipStream_t s, const HaloArgs& a, unsigned ntiles) {
   constexpr int AFL = CH * KS * KS * 2 * BM;
   const size_t lds = (size_t)2 * (AFL + 2 * CH * a.XPC) * sizeof(float);
   dim3 grid(ntiles, (a.Cout + BM - 1) / BM);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<KS, BM, CH>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_halo_kernel<KS, BM, CH, BNP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_halo_kernel<KS, BM, CH>), grid, dim3(256), lds, s, a);
+  hipLaunchKernelGGL((conv_halo_kernel<KS, BM, CH, BNP>), grid, dim3(256), lds, s, a);
 }
 
 }  // namespace
@@ -246,8 +248,17 @@ bool conv_halo_forward(hipStream_t s, const View& out, const View& in0, const Vi
   const int H = in0.H, W = in0.W;
   if (out.H != H || out.W != W || W > 128 || 128 % W != 0) return false;
   HaloArgs a{};
-  a.TH = std::min(H, 128 / W);
-  a.NP = 128 / (a.TH * W);
+  const int P = out.B * out.T;
+  const int bm = w.hbm;
+  // small pixel counts (4x4 / 8x8 levels): 32-pixel tiles so the grid still fills 256 CUs
+  int bnp = 128;
+  {
+    const int th = std::min(H, 128 / W), np = 128 / (th * W);
+    const long blocks128 = (long)((P + np - 1) / np) * ((H + th - 1) / th) * ((out.C + bm - 1) / bm);
+    if (bm == 128 && W <= 32 && blocks128 < 512) bnp = 32;
+  }
+  a.TH = std::min(H, bnp / W);
+  a.NP = bnp / (a.TH * W);
   a.RS = W + ks - 1;
   a.XPC = a.NP * (a.TH + ks - 1) * a.RS;
   const int xmax = ks == 1 ? 128 : (ks == 3 ? 288 : 560);
@@ -255,16 +266,21 @@ bool conv_halo_forward(hipStream_t s, const View& out, const View& in0, const Vi
   a.in0 = in0.p; a.i0b = in0.sb; a.i0c = in0.sc; a.i0t = in0.st; a.C0 = in0.C;
   if (in1) { a.in1 = in1->p; a.i1b = in1->sb; a.i1c = in1->sc; a.i1t = in1->st; a.Cin = in0.C + in1->C; }
   else { a.in1 = in0.p; a.i1b = in0.sb; a.i1c = in0.sc; a.i1t = in0.st; a.Cin = in0.C; }
-  a.H = H; a.W = W; a.T = out.T; a.P = out.B * out.T;
+  a.H = H; a.W = W; a.T = out.T; a.P = P;
   a.w = w.wh; a.stages = w.hstages;
   a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
   a.nrow_tiles = (H + a.TH - 1) / a.TH;
   a.e = epi;
   const unsigned ntiles = (unsigned)(((a.P + a.NP - 1) / a.NP) * a.nrow_tiles);
-  const int bm = w.hbm;
-  if (ks == 1) { if (bm == 128) launch<1, 128, 8>(s, a, ntiles); else launch<1, 64, 8>(s, a, ntiles); }
-  else if (ks == 3) { if (bm == 128) launch<3, 128, 2>(s, a, ntiles); else launch<3, 64, 4>(s, a, ntiles); }
-  else if (ks == 7) { if (bm == 128) launch<7, 128, 1>(s, a, ntiles); else launch<7, 64, 1>(s, a, ntiles); }
+#define HALO_GO(K, BMv, CHv)                                                         \
+  do {                                                                               \
+    if (bnp == 32) launch<K, BMv, CHv, 32>(s, a, ntiles);                            \
+    else launch<K, BMv, CHv, 128>(s, a, ntiles);                                     \
+  } while (0)
+  if (ks == 1) { if (bm == 128) HALO_GO(1, 128, 8); else launch<1, 64, 8, 128>(s, a, ntiles); }
+  else if (ks == 3) { if (bm == 128) HALO_GO(3, 128, 2); else launch<3, 64, 4, 128>(s, a, ntiles); }
+  else if (ks == 7) { if (bm == 128) HALO_GO(7, 128, 1); else launch<7, 64, 1, 128>(s, a, ntiles); }
+#undef HALO_GO
   else return false;
   return true;
 }

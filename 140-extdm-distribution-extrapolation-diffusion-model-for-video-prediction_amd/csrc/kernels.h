@@ -98,6 +98,11 @@ void window_attention(hipStream_t s, const View& qkv, const View& o, const AttnG
 bool stw_fused(hipStream_t s, const View& x, const AttnGeom& g, int heads, const float* gamma, const float* wqkv,
                const float* wp, const float* bp, const float* bias_dense, const float* rcos, const float* rsin,
                float q_scale);
+// Fused init_temporal_attn (double LayerNorm, qkv, temporal attention with T5 bias and
+// RoPE over frames, to_out, double residual); out must share x's strides.
+bool temporal_fused(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, const float* gamma,
+                    const float* ln_w, const float* ln_b, const float* wqkv, const float* wout,
+                    const float* bias_dense, const float* rcos, const float* rsin, float q_scale);
 // TrajWarp cross-attention (u12:719-773): q [B][256][NQ], k,v [B][256][NK].
 void cross_attention(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,
                      int heads, int NQ, int NK);

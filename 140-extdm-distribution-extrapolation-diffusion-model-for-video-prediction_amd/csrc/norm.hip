@@ -117,30 +117,56 @@ __device__ __forceinline__ float ld2(const float* p0, long b0, long c0s, int C0,
   return c < C0 ? p0[b0 + (long)c * c0s] : p1[b1 + (long)(c - C0) * c1s];
 }
 
+// 32 pixels per block, 8 channel groups per pixel (thread = (pixel, group)), so a
+// LayerNorm over hundreds of channels at few pixels still fills the machine.
 __global__ __launch_bounds__(256) void channel_ln_kernel(float* out, long osb, long osc, long ost,
                                                          const float* p0, long sb0, long sc0, long st0, int C0,
                                                          const float* p1, long sb1, long sc1, long st1, int C,
                                                          int T, int HW, int B, const float* gamma) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  __shared__ double red[8][33];
+  __shared__ float stat[2][32];
+  const int px = threadIdx.x & 31, grp = threadIdx.x >> 5;
+  const long idx = (long)blockIdx.x * 32 + px;
   const long npix = (long)B * T * HW;
-  if (idx >= npix) return;
-  const int hw = (int)(idx % HW);
-  const int t = (int)((idx / HW) % T);
-  const int b = (int)(idx / ((long)HW * T));
+  const bool ok = idx < npix;
+  const long id2 = ok ? idx : 0;
+  const int hw = (int)(id2 % HW);
+  const int t = (int)((id2 / HW) % T);
+  const int b = (int)(id2 / ((long)HW * T));
   const long b0 = (long)b * sb0 + (long)t * st0 + hw;
   const long b1 = (long)b * sb1 + (long)t * st1 + hw;
   double s = 0.0;
-  for (int c = 0; c < C; ++c) s += ld2(p0, b0, sc0, C0, p1, b1, sc1, c);
-  const double mean = s / C;
-  double v2 = 0.0;
-  for (int c = 0; c < C; ++c) {
-    const double d = ld2(p0, b0, sc0, C0, p1, b1, sc1, c) - mean;
-    v2 += d * d;
+  if (ok)
+    for (int c = grp; c < C; c += 8) s += ld2(p0, b0, sc0, C0, p1, b1, sc1, c);
+  red[grp][px] = s;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    double tt = 0.0;
+    for (int i = 0; i < 8; ++i) tt += red[i][threadIdx.x];
+    stat[0][threadIdx.x] = (float)(tt / C);
+    red[0][32] = 0.0;
   }
-  const float m = (float)mean;
-  const float den = sqrtf((float)(v2 / C) + 1e-5f);
+  __syncthreads();
+  const double mean = (double)stat[0][px];
+  double v2 = 0.0;
+  if (ok)
+    for (int c = grp; c < C; c += 8) {
+      const double d = ld2(p0, b0, sc0, C0, p1, b1, sc1, c) - mean;
+      v2 += d * d;
+    }
+  __syncthreads();
+  red[grp][px] = v2;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    double tt = 0.0;
+    for (int i = 0; i < 8; ++i) tt += red[i][threadIdx.x];
+    stat[1][threadIdx.x] = sqrtf((float)(tt / C) + 1e-5f);
+  }
+  __syncthreads();
+  if (!ok) return;
+  const float m = stat[0][px], den = stat[1][px];
   const long ob = (long)b * osb + (long)t * ost + hw;
-  for (int c = 0; c < C; ++c) {
+  for (int c = grp; c < C; c += 8) {
     const float x = ld2(p0, b0, sc0, C0, p1, b1, sc1, c);
     out[ob + (long)c * osc] = (x - m) / den * gamma[c];
   }
@@ -314,7 +340,7 @@ void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, c
 void channel_ln(hipStream_t s, const View& out, const View& in0, const View* in1, const float* gamma) {
   const View& i1 = in1 ? *in1 : in0;
   const long npix = (long)out.B * out.T * out.HW();
-  hipLaunchKernelGGL(channel_ln_kernel, dim3(nblk(npix)), dim3(256), 0, s, out.p, out.sb, out.sc, out.st, in0.p,
+  hipLaunchKernelGGL(channel_ln_kernel, dim3((unsigned)((npix + 31) / 32)), dim3(256), 0, s, out.p, out.sb, out.sc, out.st, in0.p,
                      in0.sb, in0.sc, in0.st, in0.C, i1.p, i1.sb, i1.sc, i1.st, out.C, out.T, out.HW(), out.B, gamma);
 }
 

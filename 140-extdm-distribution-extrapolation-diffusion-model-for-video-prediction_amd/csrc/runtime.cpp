@@ -451,7 +451,19 @@ struct ExtdmHandle {
     }
     // init_temporal_attn (u12:903-915, 236-327)
     View xt = alloc_cf(B, d0, T, L, L);
-    {
+    if (fused_stw_ok(d0) && T <= 32) {
+      const std::string a = "init_temporal_attn.fn.fn.fn";
+      float* wq = packed_stw_qkv(a + ".attn.to_qkv.weight");
+      float* wo = packed_stw_proj(a + ".attn.to_out.weight");
+      if (!plan) {
+        AttnGeom g{};
+        g.mode = 1; g.D = T; g.H = L; g.W = L;
+        REQUIRE(temporal_fused(s, r, xt, g, cfg.heads, D("init_temporal_attn.fn.norm.gamma"), D(a + ".norm.weight"),
+                               D(a + ".norm.bias"), wq, wo, time_bias, rope_cos, rope_sin,
+                               1.0f / std::sqrt((float)cfg.dim_head)),
+                "fused temporal attention launch rejected");
+      }
+    } else {
       Scope sc(arena);
       const std::string a = "init_temporal_attn.fn.fn.fn";
       const int hid = cfg.heads * 32;
