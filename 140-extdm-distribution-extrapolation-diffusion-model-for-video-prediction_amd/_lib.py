@@ -21,7 +21,10 @@ class ExtdmConfig(ctypes.Structure):
                 ('dim_mults', ctypes.c_int * 4), ('n_levels', ctypes.c_int), ('window', ctypes.c_int * 3),
                 ('heads', ctypes.c_int), ('dim_head', ctypes.c_int), ('tc', ctypes.c_int), ('tp', ctypes.c_int),
                 ('latent', ctypes.c_int), ('fea_size', ctypes.c_int), ('fea_ch', ctypes.c_int),
-                ('timesteps', ctypes.c_int), ('max_batch', ctypes.c_int), ('device', ctypes.c_int)]
+                ('timesteps', ctypes.c_int), ('max_batch', ctypes.c_int), ('device', ctypes.c_int),
+                ('image', ctypes.c_int), ('num_channels', ctypes.c_int), ('gen_block_expansion', ctypes.c_int),
+                ('gen_max_features', ctypes.c_int), ('gen_num_down_blocks', ctypes.c_int),
+                ('gen_num_bottleneck_blocks', ctypes.c_int)]
 
 
 _lib = None
@@ -57,7 +60,7 @@ def load():
     L.extdm_sampler_step.restype = i32
     L.extdm_bench_layer.argtypes = [vp, i32, i32, i32, ctypes.POINTER(f32), ctypes.POINTER(ctypes.c_double)]
     L.extdm_bench_layer.restype = i32
-    L.extdm_decode.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]
+    L.extdm_decode.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]
     L.extdm_decode.restype = i32
     _lib = L
     return L
@@ -90,7 +93,7 @@ def _require_device(*tensors):
 class Handle:
     """One native model instance (Unet3D weights + diffusion buffers [+ decoder])."""
 
-    def __init__(self, ucfg, timesteps, max_batch, device=0):
+    def __init__(self, ucfg, timesteps, max_batch, device=0, gcfg=None):
         L = load()
         c = ExtdmConfig()
         c.arch = 0
@@ -111,6 +114,15 @@ class Handle:
         c.timesteps = timesteps
         c.max_batch = max_batch
         c.device = device
+        if gcfg is None:
+            from .spec import GeneratorConfig
+            gcfg = GeneratorConfig(image=2 * ucfg.latent)
+        c.image = gcfg.image
+        c.num_channels = gcfg.num_channels
+        c.gen_block_expansion = gcfg.block_expansion
+        c.gen_max_features = gcfg.max_features
+        c.gen_num_down_blocks = gcfg.num_down_blocks
+        c.gen_num_bottleneck_blocks = gcfg.num_bottleneck_blocks
         self.cfg = ucfg
         self.max_batch = max_batch
         self.timesteps = timesteps
@@ -169,8 +181,10 @@ class Handle:
         check(load().extdm_bench_layer(self.h, B, layer, iters, ctypes.byref(ms), ctypes.byref(fl)))
         return float(ms.value), float(fl.value)
 
-    def decode(self, ref, flow, out):
-        _require_device(ref, flow, out)
+    def decode(self, ref, flow, out, occ=None, warped=None):
+        """ref (B,C,S,S), flow (B,2,T,fh,fw), occ (B,1,T,fh,fw) or None -> out (B,C,T,S,S)."""
+        _require_device(ref, flow, out, occ, warped)
         B, C, S, _ = ref.shape
         T, fh, fw = flow.shape[2], flow.shape[3], flow.shape[4]
-        check(load().extdm_decode(self.h, B, C, T, S, fh, fw, _ptr(ref), _ptr(flow), _ptr(out), _stream()))
+        check(load().extdm_decode(self.h, B, C, T, S, fh, fw, _ptr(ref), _ptr(flow), _ptr(occ), _ptr(out),
+                                  _ptr(warped), _stream()))

@@ -199,7 +199,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
         float v = acc[i][j][r];
         if (a.e.bias) v += a.e.bias[m];
         if (a.e.res) v += a.e.res[rbase + (long)m * a.e.res_sc];
-        if (a.e.post_scale) v = v * a.e.post_scale[(long)b * a.Cout + m] + a.e.post_shift[(long)b * a.Cout + m];
+        if (a.e.post_scale) {
+          const long pi = a.e.post_per_channel ? (long)m : (long)b * a.Cout + m;
+          v = v * a.e.post_scale[pi] + a.e.post_shift[pi];
+        }
         v = act_apply(v, a.e.act);
         a.out[obase + (long)m * a.oc] = v;
       }

@@ -54,8 +54,9 @@ struct ConvEpi {
   const float* bias = nullptr;     // [Cout]
   const float* res = nullptr;      // residual view (same B,T,H,W as out)
   long res_sb = 0, res_sc = 0, res_st = 0;
-  const float* post_scale = nullptr;  // [B][Cout]: v = v * s + sh (after bias/res)
+  const float* post_scale = nullptr;  // [B][Cout] (or [Cout] if post_per_channel): v = v * s + sh (after bias/res)
   const float* post_shift = nullptr;
+  int post_per_channel = 0;
   int act = ACT_NONE;
 };
 
@@ -131,6 +132,12 @@ void fill_normal(hipStream_t s, float* x, int B, int n, uint64_t seed, int sampl
 void set_t_from_step(hipStream_t s, int* t_batch, int B, const StepCoef* coefs, const int* step_ctr);
 void incr_counter(hipStream_t s, int* ctr);
 void t_to_int(hipStream_t s, const int64_t* t, int* t_batch, int B);
+
+// LFAE decoder pieces (decoder.hip)
+void warp_blend(hipStream_t s, float* out, const float* src, int N, int C, int S, const float* flow,
+                const float* occ, int T, int fh, int fw, const float* prev);
+void affine_relu(hipStream_t s, float* out, const float* in, const float* a, const float* b, int N, int C, int HW);
+void avgpool2(hipStream_t s, float* out, const float* in, int planes, int Ho, int Wo);
 
 // LFAE decoder (no occlusion): flow [B][2][T][h][w] (x,y) -> bilinear to
 // image size, grid_sample(src) (align_corners=True, zeros)

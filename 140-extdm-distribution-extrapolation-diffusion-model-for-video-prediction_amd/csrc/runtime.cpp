@@ -238,7 +238,7 @@ struct ExtdmHandle {
   // ---------------------------------------------------------------- op shims
   void conv(const View& out, const View& in0, const View* in1, const PackedW& w, int stride, int pad,
             const float* bias, const View* res = nullptr, int act = ACT_NONE, const float* ps = nullptr,
-            const float* psh = nullptr) {
+            const float* psh = nullptr, int per_channel = 0) {
     REQUIRE((in1 ? in0.C + in1->C : in0.C) * w.KH * w.KW == w.K || w.mode == MODE_DECONV,
             "conv: input channels do not match the weight");
     REQUIRE(out.C == w.M, "conv: output channels do not match the weight");
@@ -249,6 +249,7 @@ struct ExtdmHandle {
     e.act = act;
     e.post_scale = ps;
     e.post_shift = psh;
+    e.post_per_channel = per_channel;
     conv_forward(s, out, in0, in1, w, stride, pad, e);
   }
 
@@ -554,6 +555,140 @@ struct ExtdmHandle {
     }
   }
 
+  // ------------------------------------------------------------ LFAE decoder
+  // Eval BatchNorm as a per-channel affine: alpha = w / sqrt(rv + eps), beta = b - rm * alpha.
+  std::pair<float*, float*> bn(const std::string& p) {
+    auto it = dev.find(p + "#bn_a");
+    if (it != dev.end()) return {it->second, dev.at(p + "#bn_b")};
+    const auto& w = H(p + ".weight").f;
+    const auto& b = H(p + ".bias").f;
+    const auto& rm = H(p + ".running_mean").f;
+    const auto& rv = H(p + ".running_var").f;
+    std::vector<float> a(w.size()), bb(w.size());
+    for (size_t i = 0; i < w.size(); ++i) {
+      volatile float inv = 1.0f / std::sqrt(rv[i] + 1e-5f);
+      a[i] = inv * w[i];
+      volatile float t = rm[i] * a[i];
+      bb[i] = b[i] - t;
+    }
+    float* da = dmalloc(a.size() * 4);
+    float* db = dmalloc(bb.size() * 4);
+    HIPCHK(hipMemcpy(da, a.data(), a.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(db, bb.data(), bb.size() * 4, hipMemcpyHostToDevice));
+    dev[p + "#bn_a"] = da;
+    dev[p + "#bn_b"] = db;
+    return {da, db};
+  }
+  bool has_decoder() const { return has("generator.first.conv.weight"); }
+  bool has_unet() const { return has("init_conv.weight"); }
+
+  // conv + bias, then BN(eval) + ReLU in the epilogue (SameBlock2d / DownBlock2d / UpBlock2d)
+  void conv_bn_relu(const std::string& p, const View& out, const View& in, int pad, bool up2 = false) {
+    auto ab = bn(p + ".norm");
+    if (up2) {
+      const PackedW& w = Pup2(p + ".conv.weight");
+      conv(out, in, nullptr, w, 1, 1, D(p + ".conv.bias"), nullptr, ACT_RELU, ab.first, ab.second, 1);
+    } else {
+      conv(out, in, nullptr, P(p + ".conv.weight"), 1, pad, D(p + ".conv.bias"), nullptr, ACT_RELU, ab.first,
+           ab.second, 1);
+    }
+  }
+  const PackedW& Pup2(const std::string& n) {
+    auto it = packed.find(n + "#up2");
+    if (it != packed.end()) return it->second;
+    PackedW pw = P(n);
+    pw.mode = MODE_UP2;
+    pw.wh = nullptr;
+    return packed[n + "#up2"] = pw;
+  }
+
+  // Generator.forward_with_flow for B clips x T frames (generator.py:152-206, skips=True)
+  void decode(int B, int T, int S, int fh, int fw, const float* ref, const float* flow, const float* occ,
+              float* pred, float* warped) {
+    const int C = cfg.num_channels;
+    const int N = B * T;
+    if (!occ) {
+      // occlusion_map=None: every apply_optical returns the warped skip, so the
+      // prediction is exactly deform(source)
+      if (!plan) {
+        warp_blend(s, pred, ref, N, C, S, flow, nullptr, T, fh, fw, nullptr);
+        if (warped) warp_blend(s, warped, ref, N, C, S, flow, nullptr, T, fh, fw, nullptr);
+      }
+      return;
+    }
+    REQUIRE(has_decoder(), "decoder weights (generator.*) not loaded");
+    Scope top(arena);
+    const std::string g = "generator.";
+    const int be = cfg.gen_block_expansion, mf = cfg.gen_max_features, nd = cfg.gen_num_down_blocks;
+    // encoder half: the same source image for every frame -> once per clip
+    View vref = cf_view(const_cast<float*>(ref), B, C, 1, S, S);
+    std::vector<View> skips;
+    View e0 = alloc_cf(B, be, 1, S, S);
+    conv_bn_relu(g + "first", e0, vref, 3);
+    skips.push_back(e0);
+    View cur = e0;
+    int Sc = S;
+    for (int i = 0; i < nd; ++i) {
+      const int co = std::min(mf, be << (i + 1));
+      View t = alloc_cf(B, co, 1, Sc, Sc);
+      conv_bn_relu(g + "down_blocks." + std::to_string(i), t, cur, 1);
+      View pl = alloc_cf(B, co, 1, Sc / 2, Sc / 2);
+      if (!plan) avgpool2(s, pl.p, t.p, B * co, Sc / 2, Sc / 2);
+      skips.push_back(pl);
+      cur = pl;
+      Sc /= 2;
+    }
+    // per frame: warp the bottleneck, blend with occlusion
+    const int cb = cur.C;
+    View o = alloc_cf(N, cb, 1, Sc, Sc);
+    if (!plan) warp_blend(s, o.p, cur.p, N, cb, Sc, flow, occ, T, fh, fw, nullptr);
+    for (int i = 0; i < cfg.gen_num_bottleneck_blocks; ++i) {
+      Scope sc(arena);
+      const std::string p = g + "bottleneck.r" + std::to_string(i);
+      auto n1 = bn(p + ".norm1");
+      auto n2 = bn(p + ".norm2");
+      View a = alloc_cf(N, cb, 1, Sc, Sc);
+      if (!plan) affine_relu(s, a.p, o.p, n1.first, n1.second, N, cb, Sc * Sc);
+      View c1 = alloc_cf(N, cb, 1, Sc, Sc);
+      conv(c1, a, nullptr, P(p + ".conv1.weight"), 1, 1, D(p + ".conv1.bias"), nullptr, ACT_RELU, n2.first,
+           n2.second, 1);
+      conv(o, c1, nullptr, P(p + ".conv2.weight"), 1, 1, D(p + ".conv2.bias"), &o);
+    }
+    View up = o;
+    for (int i = 0; i < nd; ++i) {
+      View sk = skips[skips.size() - 1 - i];
+      View bl = alloc_cf(N, up.C, 1, Sc, Sc);
+      if (!plan) warp_blend(s, bl.p, sk.p, N, sk.C, Sc, flow, occ, T, fh, fw, up.p);
+      const int co = std::min(mf, be << (nd - i - 1));
+      View u = alloc_cf(N, co, 1, Sc * 2, Sc * 2);
+      conv_bn_relu(g + "up_blocks." + std::to_string(i), u, bl, 1, true);
+      up = u;
+      Sc *= 2;
+    }
+    View bl = alloc_cf(N, up.C, 1, Sc, Sc);
+    if (!plan) warp_blend(s, bl.p, skips[0].p, N, up.C, Sc, flow, occ, T, fh, fw, up.p);
+    View f = alloc_cf(N, C, 1, S, S);
+    conv(f, bl, nullptr, P(g + "final.weight"), 1, 3, D(g + "final.bias"), nullptr, ACT_SIGMOID);
+    // frame-major scratch -> caller layout [B][C][T][S][S] happens in warp_blend's output
+    View pr = alloc_cf(N, C, 1, S, S);
+    if (!plan) {
+      warp_blend(s, pr.p, ref, N, C, S, flow, occ, T, fh, fw, f.p);
+      copy_view(s, cf_view(pred, B, C, T, S, S), frames_as_bt(pr, B, T));
+      if (warped) {
+        warp_blend(s, f.p, ref, N, C, S, flow, nullptr, T, fh, fw, nullptr);
+        copy_view(s, cf_view(warped, B, C, T, S, S), frames_as_bt(f, B, T));
+      }
+    }
+  }
+  // view an [N = B*T][C][1][S][S] buffer as [B][C][T][S][S]
+  static View frames_as_bt(const View& v, int B, int T) {
+    View o = v;
+    o.B = B; o.T = T;
+    o.sb = v.sb * T;  // frame n = b*T + t
+    o.st = v.sb;
+    return o;
+  }
+
   // ------------------------------------------------------------ finalize
   void build_tables() {
     const int NT = cfg.timesteps;
@@ -670,21 +805,38 @@ struct ExtdmHandle {
   }
 
   void finalize() {
-    REQUIRE(cfg.dim_head == 32, "this build supports attn_dim_head == 32");
-    REQUIRE(cfg.heads % 4 == 0, "attn_heads must be a multiple of 4");
     HIPCHK(hipSetDevice(cfg.device));
     s = 0;
+    if (!has_unet()) {  // decoder-only handle
+      for (auto& kv : host)
+        if (!kv.second.is_int && kv.second.f.size() <= (1u << 16)) D(kv.first);
+      finalize_workspace();
+      return;
+    }
+    REQUIRE(cfg.dim_head == 32, "this build supports attn_dim_head == 32");
+    REQUIRE(cfg.heads % 4 == 0, "attn_heads must be a multiple of 4");
     // small tensors (biases, norm gains) go to the device now so that no
     // host->device copy can happen while a sampler step is being captured
     for (auto& kv : host)
       if (!kv.second.is_int && kv.second.f.size() <= (1u << 16)) D(kv.first);
     build_tables();
+    finalize_workspace();
+  }
+
+  // Size the arena by planning passes of everything the handle can run.
+  void finalize_workspace() {
     // pack every weight the forward touches by running it in planning mode
     const int B = cfg.max_batch;
     plan = true;
     arena.planning = true;
     arena.top = arena.peak = 0;
-    unet_forward(B, nullptr, nullptr, nullptr, nullptr);
+    if (has_unet()) unet_forward(B, nullptr, nullptr, nullptr, nullptr);
+    if (has_decoder()) {
+      arena.top = 0;
+      const int fl = cfg.latent > 0 ? cfg.latent : cfg.image / 2;
+      decode(B, cfg.tc + cfg.tp, cfg.image, fl, fl, nullptr, nullptr, reinterpret_cast<const float*>(16), nullptr,
+             nullptr);
+    }
     plan = false;
     arena.planning = false;
     const size_t need = arena.peak + (1 << 20);
@@ -943,12 +1095,17 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
 }
 
 int extdm_decode(ExtdmHandle* h, int B, int C, int T, int S, int fh, int fw, const float* ref, const float* flow,
-                 float* out, void* stream) {
+                 const float* occ, float* pred, float* warped, void* stream) {
   return guarded([&] {
     REQUIRE(h, "null handle");
     HIPCHK(hipSetDevice(h->cfg.device));
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    warp_frames(s, out, ref, flow, B, C, T, S, fh, fw, (long)C * T * S * S, (long)T * S * S, (long)S * S);
+    h->s = reinterpret_cast<hipStream_t>(stream);
+    if (occ) {
+      REQUIRE(h->finalized, "handle not finalized");
+      REQUIRE(B <= h->cfg.max_batch && T <= h->cfg.tc + h->cfg.tp, "decode exceeds the planned batch");
+      REQUIRE(C == h->cfg.num_channels && S == h->cfg.image, "decode geometry differs from the config");
+    }
+    h->decode(B, T, S, fh, fw, ref, flow, occ, pred, warped);
     HIPCHK(hipGetLastError());
   });
 }

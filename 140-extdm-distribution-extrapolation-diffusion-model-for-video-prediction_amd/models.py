@@ -267,29 +267,40 @@ class Generator(nn.Module):
         _register_tree(self, spec, synth_state_dict(spec, seed=seed))
         self._handle = None
 
-    def _h(self, device):
-        if self._handle is None:
-            ucfg = UnetConfig()
-            self._handle = _lib.Handle(ucfg, 1000, 1, device.index or 0)
-        return self._handle
+    def _h(self, device, B, T):
+        """Native decoder handle sized for B clips x T frames (rebuilt when exceeded)."""
+        key = (device.index or 0,)
+        h = self._handle
+        if h is None or h[0] != key or h[1] < B or h[2] < T or h[3] != self._state_version():
+            ucfg = UnetConfig(tc=1, tp=max(T, 2) - 1, latent=self.gcfg.image // 2)
+            nh = _lib.Handle(ucfg, 1000, B, key[0], gcfg=self.gcfg)
+            nh.load_state({'generator.' + k: v for k, v in self.state_dict().items()})
+            nh.finalize()
+            self._handle = h = (key, B, max(T, 2), self._state_version(), nh)
+        return h[4]
+
+    def _state_version(self):
+        return tuple((p.data_ptr(), p._version) for p in self.parameters())
 
     @torch.no_grad()
     def forward_with_flow(self, source_image, optical_flow, occlusion_map):
-        """optical_flow: (B, h, w, 2) like the reference. Returns the reference's
-        output dict keys 'prediction' and 'deformed'."""
-        if occlusion_map is not None:
-            raise NotImplementedError('the occlusion-blended decoder is not native yet (BAIR/KTH/SMMNIST eval '
-                                      'scripts run with estimate_occlusion_map=False)')
-        out = self.decode_frames(source_image, optical_flow.permute(0, 3, 1, 2)[:, :, None])
-        pred = out[:, :, 0]
-        return {'prediction': pred, 'deformed': pred.clone()}
+        """Reference signature (generator.py:152): optical_flow (B, h, w, 2),
+        occlusion_map (B, 1, h, w) or None. Returns 'prediction' and 'deformed'."""
+        flow = optical_flow.permute(0, 3, 1, 2)[:, :, None]
+        occ = occlusion_map[:, :, None] if occlusion_map is not None else None
+        pred, warped = self.decode_frames(source_image, flow, occ, with_warped=True)
+        return {'prediction': pred[:, :, 0], 'deformed': warped[:, :, 0]}
 
     @torch.no_grad()
-    def decode_frames(self, source_image, flow):
-        """All frames at once: source_image (B,C,S,S), flow (B,2,T,h,w) -> (B,C,T,S,S)."""
+    def decode_frames(self, source_image, flow, occ=None, with_warped=False):
+        """All frames at once: source_image (B,C,S,S), flow (B,2,T,h,w), occ (B,1,T,h,w)
+        or None -> prediction (B,C,T,S,S) [, deformed]."""
         src = source_image.float().contiguous()
         fl = flow.float().contiguous()
+        oc = occ.float().contiguous() if occ is not None else None
         B, C, S, _ = src.shape
-        out = torch.empty(B, C, fl.shape[2], S, S, device=src.device, dtype=torch.float32)
-        self._h(src.device).decode(src, fl, out)
-        return out
+        T = fl.shape[2]
+        pred = torch.empty(B, C, T, S, S, device=src.device, dtype=torch.float32)
+        warped = torch.empty_like(pred) if with_warped else None
+        self._h(src.device, B, T).decode(src, fl, pred, occ=oc, warped=warped)
+        return (pred, warped) if with_warped else pred

@@ -50,8 +50,10 @@ typedef struct ExtdmConfig {
   int fea_size;        /* cond_fea H = W (16) */
   int fea_ch;          /* cond_fea channels (256) */
   int timesteps;       /* diffusion T (1000) */
-  int max_batch;       /* workspace is sized for this batch */
+  int max_batch;       /* workspace is sized for this batch (clips) */
   int device;          /* HIP device ordinal */
+  /* LFAE Generator decoder (flow_params.generator_params); image = frame size */
+  int image, num_channels, gen_block_expansion, gen_max_features, gen_num_down_blocks, gen_num_bottleneck_blocks;
 } ExtdmConfig;
 
 int extdm_create(const ExtdmConfig* cfg, ExtdmHandle** out);
@@ -91,10 +93,13 @@ int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, fl
  * launch and the algorithmic FLOPs per launch. */
 int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out, double* flops_out);
 
-/* LFAE decoder for occlusion_map=None: prediction (== deformed) of every frame.
- * ref: [B,C,S,S]; flow: [B,2,T,fh,fw] (x, y); out: [B,C,T,S,S]. */
+/* LFAE decoder (Generator.forward_with_flow) for B clips x T frames.
+ * ref: [B,C,S,S] source image; flow: [B,2,T,fh,fw] (x, y grid); occ: [B,1,T,fh,fw]
+ * occlusion in [0,1] or NULL (reference quirk: without occlusion the prediction
+ * equals the warped source); pred: [B,C,T,S,S]; warped: [B,C,T,S,S] or NULL
+ * ('deformed'). Needs the decoder weights (keys 'generator.*') unless occ is NULL. */
 int extdm_decode(ExtdmHandle* h, int B, int C, int T, int S, int fh, int fw, const float* ref, const float* flow,
-                 float* out, void* stream);
+                 const float* occ, float* pred, float* warped, void* stream);
 
 #ifdef __cplusplus
 }

@@ -187,6 +187,33 @@ def test_decoder_no_occlusion_vs_reference_golden():
     assert torch.equal(out['prediction'], out['deformed'])
 
 
+def test_decoder_with_occlusion_vs_reference_golden():
+    """Full Generator.forward_with_flow: encoder half, warped bottleneck, 6 ResBlock2d,
+    occlusion-blended skips, nearest-x2 up blocks, sigmoid head (generator.py:152-206)."""
+    src, flow, occ = decoder_inputs()
+    g = load('decoder.npz')
+    gen = pkg.Generator()
+    gen.load_state_dict(make_gen_sd())
+    out = gen.forward_with_flow(src.to(DEV), flow.to(DEV), occ.to(DEV))
+    err = np.abs(out['prediction'].cpu().numpy() - g['pred_occ']).max()
+    assert err <= 1e-4, err
+    err_d = np.abs(out['deformed'].cpu().numpy() - g['deformed']).max()
+    assert err_d <= 1e-5, err_d
+
+
+def test_decoder_multi_frame_matches_per_frame():
+    """decode_frames over T frames == T single-frame calls (encoder half hoisted)."""
+    src, flow, occ = decoder_inputs()
+    gen = pkg.Generator()
+    gen.load_state_dict(make_gen_sd())
+    fl = torch.stack([flow.permute(0, 3, 1, 2), flow.flip(1).permute(0, 3, 1, 2)], dim=2).to(DEV)
+    oc = torch.stack([occ, 1 - occ], dim=2).to(DEV)
+    allf = gen.decode_frames(src.to(DEV), fl, oc)
+    for t in range(2):
+        one = gen.decode_frames(src.to(DEV), fl[:, :, t:t + 1].contiguous(), oc[:, :, t:t + 1].contiguous())
+        assert (allf[:, :, t] - one[:, :, 0]).abs().max().item() <= 1e-6
+
+
 def test_drop_in_api_sample_shapes_and_determinism():
     cfg = CONFIGS['small']
     u = pkg.Unet3D(dim=cfg.dim, channels=512, dim_mults=cfg.dim_mults, cond_num=cfg.tc, pred_num=cfg.tp,
