@@ -4,4 +4,5 @@ Import with importlib (the directory name is not a Python identifier):
     pkg = importlib.import_module('140-extdm-distribution-extrapolation-diffusion-model-for-video-prediction_amd')
 """
 from . import spec, weights, _lib  # noqa: F401
-from .models import Unet3D, GaussianDiffusion, Generator, schedule_buffers, ddim_time_pairs  # noqa: F401
+from .models import (Unet3D, Unet3DAda, Unet3DAdaU22, Unet3DWoRef, UNET3D_BY_MODULE, GaussianDiffusion,  # noqa: F401
+                     Generator, schedule_buffers, ddim_time_pairs)

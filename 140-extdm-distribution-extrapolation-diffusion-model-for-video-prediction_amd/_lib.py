@@ -96,7 +96,8 @@ class Handle:
     def __init__(self, ucfg, timesteps, max_batch, device=0, gcfg=None):
         L = load()
         c = ExtdmConfig()
-        c.arch = 0
+        from .spec import ARCH_IDS
+        c.arch = ARCH_IDS[ucfg.arch]
         c.dim = ucfg.dim
         c.channels = ucfg.channels
         mults = list(ucfg.dim_mults)

@@ -90,20 +90,26 @@ struct AttnGeom {
   int ss0, ss1, ss2; // effective shift
   int Dp, Hp, Wp;    // padded extents
 };
+// Unfused attention (dim_head 32, <= 32 tokens per group; e.g. C = 512 levels).
 // qkv: channel-first [B][3*heads*32][T][H][W]; o: [B][heads*32][T][H][W].
 void window_attention(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads,
                       const float* bias_dense /*[heads][32][32]*/, const float* rope_cos,
-                      const float* rope_sin /*[32][16]*/, float q_scale);
+                      const float* rope_sin /*[>=32][16]*/, float q_scale);
+// Shapes the fused attention kernels handle: heads 8, C in {64,128,256}, a group of
+// <= 32 or exactly 64 tokens, dim_head 16 or 32.
+bool fused_attn_supported(int C, int ntok, int dim_head, int heads);
 // Fused Residual(PreNorm(STWAttentionLayer)) in place on x (stw_fused.hip); false if
-// C not in {64,128,256} or heads != 8. Weights pre-packed (see the kernel header).
-bool stw_fused(hipStream_t s, const View& x, const AttnGeom& g, int heads, const float* gamma, const float* wqkv,
-               const float* wp, const float* bp, const float* bias_dense, const float* rcos, const float* rsin,
-               float q_scale);
-// Fused init_temporal_attn (double LayerNorm, qkv, temporal attention with T5 bias and
-// RoPE over frames, to_out, double residual); out must share x's strides.
-bool temporal_fused(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, const float* gamma,
-                    const float* ln_w, const float* ln_b, const float* wqkv, const float* wout,
-                    const float* bias_dense, const float* rcos, const float* rsin, float q_scale);
+// the shape is unsupported. Weights pre-packed (see the kernel header);
+// bias_dense [heads][bstride][bstride]; rope tables [64][dim_head/2].
+bool stw_fused(hipStream_t s, const View& x, const AttnGeom& g, int heads, int dim_head, const float* gamma,
+               const float* wqkv, const float* wp, const float* bp, const float* bias_dense, int bstride,
+               const float* rcos, const float* rsin, float q_scale);
+// Fused Residual(PreNorm(chanLN, AttentionLayer)) over frames (double LayerNorm, qkv,
+// temporal attention with T5 bias and RoPE, to_out, double residual); out must share
+// x's strides and may alias x.
+bool temporal_fused(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, int dim_head,
+                    const float* gamma, const float* ln_w, const float* ln_b, const float* wqkv, const float* wout,
+                    const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale);
 // TrajWarp cross-attention (u12:719-773): q [B][256][NQ], k,v [B][256][NK].
 void cross_attention(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,
                      int heads, int NQ, int NK);

@@ -184,6 +184,26 @@ struct ExtdmHandle {
     pw.hstages = stages;
     pw.hbm = bm;
   }
+  // Conv3d weight W[co][ci][3][kh][kw] as a (1,kh,kw) conv over 3*ci channels
+  // ordered (kt, ci): W'[co][kt*ci + c] = W[co][c][kt].
+  const PackedW& Ptime3(const std::string& n) {
+    const std::string key = n + "#t3";
+    if (!host.count(key)) {
+      const HostTensor& t = H(n);
+      const int co = (int)t.shape[0], ci = (int)t.shape[1], kt = (int)t.shape[2];
+      const int kk = (int)(t.shape[3] * t.shape[4]);
+      HostTensor r;
+      r.shape = {co, (int64_t)kt * ci, t.shape[3], t.shape[4]};
+      r.f.resize(t.f.size());
+      for (int m = 0; m < co; ++m)
+        for (int c = 0; c < ci; ++c)
+          for (int z = 0; z < kt; ++z)
+            for (int q = 0; q < kk; ++q)
+              r.f[(((size_t)m * kt * ci) + (size_t)z * ci + c) * kk + q] = t.f[(((size_t)m * ci + c) * kt + z) * kk + q];
+      host[key] = std::move(r);
+    }
+    return P(key);
+  }
   // ConvTranspose3d(1,4,4)/s2/p1 weight W[ci][co][1][4][4] -> four 2x2 parity GEMMs:
   // parity (py,px) tap (ky',kx') uses W[..][3-py-2ky'][3-px-2kx'].
   const PackedW& Pdeconv(const std::string& n) {
@@ -297,19 +317,21 @@ struct ExtdmHandle {
     return g;
   }
 
-  // Packed weights of the fused STW kernel (stw_fused.hip header).
+  // Packed weights of the fused attention kernels (stw_fused.hip header): qkv rows
+  // in 32-row units (one head of dim 32 / two heads of dim 16).
   float* packed_stw_qkv(const std::string& n) {
     auto it = dev.find(n + "#stwqkv");
     if (it != dev.end()) return it->second;
     const HostTensor& t = H(n);
-    const int C = (int)t.shape[1], heads = cfg.heads;
-    std::vector<float> a((size_t)heads * (C / 2) * 3 * 64);
-    for (int hd = 0; hd < heads; ++hd)
+    const int C = (int)t.shape[1], hid = cfg.heads * cfg.dim_head, units = hid / 32;
+    REQUIRE((int)t.shape[0] == 3 * hid, "qkv weight rows != 3 * heads * dim_head: " + n);
+    std::vector<float> a((size_t)units * (C / 2) * 3 * 64);
+    for (int u = 0; u < units; ++u)
       for (int s2 = 0; s2 < C / 2; ++s2)
         for (int wh = 0; wh < 3; ++wh)
           for (int l = 0; l < 64; ++l)
-            a[(((size_t)hd * (C / 2) + s2) * 3 + wh) * 64 + l] =
-                t.f[(size_t)(wh * heads * 32 + hd * 32 + (l & 31)) * C + 2 * s2 + (l >> 5)];
+            a[(((size_t)u * (C / 2) + s2) * 3 + wh) * 64 + l] =
+                t.f[(size_t)(wh * hid + u * 32 + (l & 31)) * C + 2 * s2 + (l >> 5)];
     float* d = dmalloc(a.size() * 4);
     HIPCHK(hipMemcpy(d, a.data(), a.size() * 4, hipMemcpyHostToDevice));
     return dev[n + "#stwqkv"] = d;
@@ -328,24 +350,34 @@ struct ExtdmHandle {
     HIPCHK(hipMemcpy(d, a.data(), a.size() * 4, hipMemcpyHostToDevice));
     return dev[n + "#stwproj"] = d;
   }
-  bool fused_stw_ok(int C) const {
+  bool fused_ok(int C, int ntok) const {
     static const bool off = [] { const char* v = getenv("EXTDM_NO_FUSED_STW"); return v && v[0] && v[0] != '0'; }();
-    return !off && cfg.heads == 8 && cfg.dim_head == 32 && (C == 64 || C == 128 || C == 256);
+    return !off && fused_attn_supported(C, ntok, cfg.dim_head, cfg.heads);
   }
+  float q_scale() const { return 1.0f / std::sqrt((float)cfg.dim_head); }
+  // model frame count: wo_ref drops the last cond frame (wo_ref.py:911)
+  int tm() const { return cfg.arch == EXTDM_ARCH_WO_REF ? cfg.tc - 1 : cfg.tc; }
+  int frames() const { return tm() + cfg.tp; }
 
   // Residual(PreNorm(STWAttentionLayer)) in place on x (u12:498-559, 961-963)
   void stw(const std::string& p, const View& x, bool shifted) {
-    if (fused_stw_ok(x.C)) {
+    const AttnGeom g = stw_geom(x.T, x.H, x.W, shifted);
+    const int N = g.ws0 * g.ws1 * g.ws2;
+    // dense bias tables are laid out for the configured window (build_tables); a
+    // collapsed window reads their leading N x N block (index[:N, :N], u12:476)
+    const int bstride = cfg.window[0] * cfg.window[1] * cfg.window[2] <= 32 ? 32 : 64;
+    if (fused_ok(x.C, N)) {
       const std::string a = p + ".fn.fn.attn";
       float* wq = packed_stw_qkv(a + ".qkv.weight");
       float* wp = packed_stw_proj(a + ".proj.weight");
       if (plan) return;
-      const AttnGeom g = stw_geom(x.T, x.H, x.W, shifted);
-      REQUIRE(stw_fused(s, x, g, cfg.heads, D(p + ".fn.norm.gamma"), wq, wp, D(a + ".proj.bias"), bias_dense.at(p),
-                        rope_cos, rope_sin, 1.0f / std::sqrt((float)cfg.dim_head)),
+      REQUIRE(stw_fused(s, x, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), wq, wp, D(a + ".proj.bias"),
+                        bias_dense.at(p), bstride, rope_cos, rope_sin, q_scale()),
               "fused STW launch rejected");
       return;
     }
+    REQUIRE(cfg.dim_head == 32 && N <= 32 && bstride == 32, "STW attention shape without a kernel (C=" + std::to_string(x.C) +
+                                               ", window tokens " + std::to_string(N) + ")");
     Scope sc(arena);
     const int hid = cfg.heads * 32;
     View ln = alloc_cf(x.B, x.C, x.T, x.H, x.W);
@@ -353,22 +385,48 @@ struct ExtdmHandle {
     View qkv = alloc_cf(x.B, 3 * hid, x.T, x.H, x.W);
     conv(qkv, ln, nullptr, P(p + ".fn.fn.attn.qkv.weight"), 1, 0, nullptr);
     View o = alloc_cf(x.B, hid, x.T, x.H, x.W);
-    const AttnGeom g = stw_geom(x.T, x.H, x.W, shifted);
-    if (!plan)
-      window_attention(s, qkv, o, g, cfg.heads, bias_dense.at(p), rope_cos, rope_sin,
-                       1.0f / std::sqrt((float)cfg.dim_head));
+    if (!plan) window_attention(s, qkv, o, g, cfg.heads, bias_dense.at(p), rope_cos, rope_sin, q_scale());
     conv(x, o, nullptr, P(p + ".fn.fn.attn.proj.weight"), 1, 0, D(p + ".fn.fn.attn.proj.bias"), &x);
   }
 
-  AdaptorGeom adaptor_geom() const {
-    const int L = std::max(1, (int)std::ceil(std::log2((double)(cfg.tp + 1) / cfg.tc)));
-    return {L, ((1 << L) - 1) * cfg.tc};
+  // Residual(PreNorm(dim, EinopsToAndFrom(AttentionLayer))) over the frames of every
+  // pixel (u12:236-327, 903-915): out = x + chanLN(x) + to_out(attn(LN(chanLN(x)))).
+  // out may alias x.
+  void temporal(const std::string& p, const View& x, const View& out) {
+    const std::string a = p + ".fn.fn.fn";
+    const int T = x.T;
+    AttnGeom g{};
+    g.mode = 1; g.D = T; g.H = x.H; g.W = x.W;
+    if (fused_ok(x.C, T) && T <= 32) {
+      float* wq = packed_stw_qkv(a + ".attn.to_qkv.weight");
+      float* wo = packed_stw_proj(a + ".attn.to_out.weight");
+      if (plan) return;
+      REQUIRE(temporal_fused(s, x, out, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), D(a + ".norm.weight"),
+                             D(a + ".norm.bias"), wq, wo, time_bias, 32, rope_cos, rope_sin, q_scale()),
+              "fused temporal attention launch rejected");
+      return;
+    }
+    REQUIRE(cfg.dim_head == 32 && T <= 32, "temporal attention shape without a kernel");
+    Scope sc(arena);
+    const int hid = cfg.heads * 32;
+    View z = alloc_cf(x.B, x.C, T, x.H, x.W), rr = alloc_cf(x.B, x.C, T, x.H, x.W);
+    if (!plan) temporal_prologue(s, x, D(p + ".fn.norm.gamma"), D(a + ".norm.weight"), D(a + ".norm.bias"), z, rr);
+    View qkv = alloc_cf(x.B, 3 * hid, T, x.H, x.W);
+    conv(qkv, z, nullptr, P(a + ".attn.to_qkv.weight"), 1, 0, nullptr);
+    View o = alloc_cf(x.B, hid, T, x.H, x.W);
+    if (!plan) window_attention(s, qkv, o, g, cfg.heads, time_bias, rope_cos, rope_sin, q_scale());
+    conv(out, o, nullptr, P(a + ".attn.to_out.weight"), 1, 0, nullptr, &rr);
   }
 
-  // MotionAdaptor in place on frames [tc, T) of x (u12:644-717)
+  AdaptorGeom adaptor_geom() const {
+    const int L = std::max(1, (int)std::ceil(std::log2((double)(cfg.tp + 1) / tm())));
+    return {L, ((1 << L) - 1) * tm()};
+  }
+
+  // MotionAdaptor in place on frames [tm, T) of x (u12:644-717; tm = tc, or tc-1 in wo_ref)
   void adaptor(const std::string& p, const View& x) {
     Scope sc(arena);
-    const int B = x.B, C = x.C, Hh = x.H, Ww = x.W, tc = cfg.tc, tp = cfg.tp, HW = Hh * Ww;
+    const int B = x.B, C = x.C, Hh = x.H, Ww = x.W, tc = tm(), tp = cfg.tp, HW = Hh * Ww;
     const AdaptorGeom ag = adaptor_geom();
     const std::string ap = p + ".adaptors";
     View E = alloc_tm(B, C, tc << ag.L, Hh, Ww);
@@ -383,14 +441,31 @@ struct ExtdmHandle {
     for (int l = 0; l < ag.L; ++l) {
       Scope s2(arena);
       const int nl = tc << l;
+      const std::string wn = ap + ".extrapolators." + std::to_string(l) + ".fn.weight";
+      const bool t3 = H(wn).shape[2] == 3;  // ada_u22: Conv3d(k=3, pad=1) (ada_u22.py:537)
       float* mean = arena.alloc((size_t)B * C);
       float* sd = arena.alloc((size_t)B * C);
       View cur = E.frames(0, nl);
       if (!plan) adaptor_stats(s, cur, mean, sd, partials);
-      View hn = alloc_tm(B, C, nl, Hh, Ww);
-      if (!plan) adaptor_normalize(s, hn, cur, mean, sd);
-      conv(E.frames(nl, nl), hn, nullptr, P(ap + ".extrapolators." + std::to_string(l) + ".fn.weight"), 1, 1,
-           nullptr, &hn, ACT_NONE, sd, mean);
+      if (!t3) {
+        View hn = alloc_tm(B, C, nl, Hh, Ww);
+        if (!plan) adaptor_normalize(s, hn, cur, mean, sd);
+        conv(E.frames(nl, nl), hn, nullptr, P(wn), 1, 1, nullptr, &hn, ACT_NONE, sd, mean);
+      } else {
+        // Frame-major buffer with one zero frame either side: in frame-major layout
+        // channel kt*C + c of frame t is channel c of frame t+kt-1, so the 3x3x3 conv
+        // is a (1,3,3) conv over 3C "channels" of a plain strided view.
+        View hp = alloc_tm(B, C, nl + 2, Hh, Ww);
+        View hn = hp.frames(1, nl);
+        if (!plan) {
+          HIPCHK(hipMemset2DAsync(hp.p, hp.sb * 4, 0, hp.st * 4, B, s));
+          HIPCHK(hipMemset2DAsync(hp.p + (size_t)(nl + 1) * hp.st, hp.sb * 4, 0, hp.st * 4, B, s));
+          adaptor_normalize(s, hn, cur, mean, sd);
+        }
+        View win = hp;
+        win.C = 3 * C; win.T = nl;
+        conv(E.frames(nl, nl), win, nullptr, Ptime3(wn), 1, 1, nullptr, &hn, ACT_NONE, sd, mean);
+      }
     }
     // Tmodulator: 1x1 conv over '(T C)' channels of the F extrapolated frames
     View ein = E.frames(tc, ag.F);
@@ -427,60 +502,57 @@ struct ExtdmHandle {
     conv(fp_out, fp, &fm2p, P("init_traj.fuser.weight"), 1, 0, D("init_traj.fuser.bias"));
   }
 
-  // Unet3D.forward (u12:1017-1086). x: [B,3,tp,L,L], cond: [B,3,tc,L,L],
-  // fea: [B,fea_ch,T,fs,fs], eps: [B,3,tp,L,L]; t_batch already on device.
+  // Unet3D.forward for the four reference denoisers (arch switch, include/extdm.h):
+  //   u12      DenoiseNet_..._traj_u12.py:1017-1086 (== u22)
+  //   ada      DenoiseNet_..._traj_ada.py:1020-1089
+  //   ada_u22  DenoiseNet_..._traj_ada_u22.py:1172-1306 (path=0)
+  //   wo_ref   DenoiseNet_..._wo_ref_adaptor_cross_multi.py:906-967
+  // x: [B,3,tp,L,L], cond: [B,3,tc,L,L], fea: [B,fea_ch,T,fs,fs] with T = tm + tp,
+  // eps: [B,3,tp,L,L]; t_batch already on device.
   void unet_forward(int B, const float* x, const float* cond, const float* fea, float* eps) {
     Scope top(arena);
-    const int tc = cfg.tc, tp = cfg.tp, T = tc + tp, L = cfg.latent, fs = cfg.fea_size, d0 = cfg.dim;
+    const int arch = cfg.arch;
+    const int tc = tm(), tp = cfg.tp, T = frames(), L = cfg.latent, fs = cfg.fea_size, d0 = cfg.dim;
+    const bool u22 = arch == EXTDM_ARCH_ADA_U22;
     View vx = cf_view(const_cast<float*>(x), B, 3, tp, L, L);
-    View vc = cf_view(const_cast<float*>(cond), B, 3, tc, L, L);
+    View vc = cf_view(const_cast<float*>(cond), B, 3, cfg.tc, L, L);
     View vf = cf_view(const_cast<float*>(fea), B, cfg.fea_ch, T, fs, fs);
     View veps = cf_view(eps, B, 3, tp, L, L);
 
-    View r = alloc_cf(B, d0, T, L, L);  // `r` of u12:1042
+    View r = alloc_cf(B, d0, T, L, L);  // `r` (u12:1042)
     {
       Scope sc(arena);
+      // cat([cond_frames (minus the last in wo_ref), x], dim=2)
       View xin = alloc_cf(B, 3, T, L, L);
-      if (!plan) { copy_view(s, xin.frames(0, tc), vc); copy_view(s, xin.frames(tc, tp), vx); }
-      View x0 = alloc_cf(B, 256, T, L, L);
-      conv(x0, xin, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
-      View fp2 = alloc_cf(B, cfg.fea_ch, tp, fs, fs);
-      trajwarp(x0, vf, fp2);
-      View fup = alloc_cf(B, cfg.fea_ch, T, L, L);
-      if (!plan) bilinear_frames(s, fup, vf, fp2, tc);
-      conv(r, x0, &fup, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
-    }
-    // init_temporal_attn (u12:903-915, 236-327)
-    View xt = alloc_cf(B, d0, T, L, L);
-    if (fused_stw_ok(d0) && T <= 32) {
-      const std::string a = "init_temporal_attn.fn.fn.fn";
-      float* wq = packed_stw_qkv(a + ".attn.to_qkv.weight");
-      float* wo = packed_stw_proj(a + ".attn.to_out.weight");
-      if (!plan) {
-        AttnGeom g{};
-        g.mode = 1; g.D = T; g.H = L; g.W = L;
-        REQUIRE(temporal_fused(s, r, xt, g, cfg.heads, D("init_temporal_attn.fn.norm.gamma"), D(a + ".norm.weight"),
-                               D(a + ".norm.bias"), wq, wo, time_bias, rope_cos, rope_sin,
-                               1.0f / std::sqrt((float)cfg.dim_head)),
-                "fused temporal attention launch rejected");
+      if (!plan) { copy_view(s, xin.frames(0, tc), vc.frames(0, tc)); copy_view(s, xin.frames(tc, tp), vx); }
+      if (arch == EXTDM_ARCH_WO_REF) {
+        // cond_fea enters at latent resolution, no feature branch (wo_ref.py:916-921)
+        REQUIRE(fs == L, "wo_ref: cond_fea must be at the latent resolution");
+        conv(r, xin, &vf, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+      } else {
+        View x0 = xin;
+        if (arch != EXTDM_ARCH_ADA_U22) {
+          x0 = alloc_cf(B, 256, T, L, L);
+          conv(x0, xin, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
+        }
+        View fup = alloc_cf(B, cfg.fea_ch, T, L, L);
+        if (arch == EXTDM_ARCH_U12) {
+          View fp2 = alloc_cf(B, cfg.fea_ch, tp, fs, fs);
+          trajwarp(x0, vf, fp2);
+          if (!plan) bilinear_frames(s, fup, vf, fp2, tc);
+        } else {
+          // cond_adaptor then cond_temporal_attn on cond_fea (ada.py:1035-1036)
+          View fa = alloc_cf(B, cfg.fea_ch, T, fs, fs);
+          if (!plan) copy_view(s, fa, vf);
+          adaptor("cond_adaptor", fa);
+          temporal("cond_temporal_attn", fa, fa);
+          if (!plan) bilinear_frames(s, fup, fa, fa, T);
+        }
+        conv(r, x0, &fup, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
       }
-    } else {
-      Scope sc(arena);
-      const std::string a = "init_temporal_attn.fn.fn.fn";
-      const int hid = cfg.heads * 32;
-      View z = alloc_cf(B, d0, T, L, L), rr = alloc_cf(B, d0, T, L, L);
-      if (!plan)
-        temporal_prologue(s, r, D("init_temporal_attn.fn.norm.gamma"), D(a + ".norm.weight"), D(a + ".norm.bias"), z,
-                          rr);
-      View qkv = alloc_cf(B, 3 * hid, T, L, L);
-      conv(qkv, z, nullptr, P(a + ".attn.to_qkv.weight"), 1, 0, nullptr);
-      View o = alloc_cf(B, hid, T, L, L);
-      AttnGeom g{};
-      g.mode = 1; g.D = T; g.H = L; g.W = L;
-      if (!plan)
-        window_attention(s, qkv, o, g, cfg.heads, time_bias, rope_cos, rope_sin, 1.0f / std::sqrt((float)cfg.dim_head));
-      conv(xt, o, nullptr, P(a + ".attn.to_out.weight"), 1, 0, nullptr, &rr);
     }
+    View xt = alloc_cf(B, d0, T, L, L);
+    temporal("init_temporal_attn", r, xt);
     // downs
     std::vector<int> dims = {d0};
     for (int i = 0; i < cfg.n_levels; ++i) dims.push_back(d0 * cfg.dim_mults[i]);
@@ -488,61 +560,86 @@ struct ExtdmHandle {
     std::vector<View> skips;
     View cur = xt;
     int Hc = L;
+    const std::string down_ix = u22 ? ".6" : ".5";
     for (int i = 0; i < nl; ++i) {
       const std::string p = "downs." + std::to_string(i);
       const int dout = dims[i + 1];
       View a1 = alloc_cf(B, dout, T, Hc, Hc);
-      resblock(p + ".0", cur, nullptr, a1);
-      stw(p + ".1", a1, true);
       View a2 = alloc_cf(B, dout, T, Hc, Hc);
-      resblock(p + ".2", a1, nullptr, a2);
-      stw(p + ".3", a2, false);
-      if (i > 1) adaptor(p + ".4", a2);
+      if (u22) {
+        // b1, b2, STW1, STW2, adaptor, temporal attention (ada_u22.py:1268-1281)
+        resblock(p + ".0", cur, nullptr, a1);
+        resblock(p + ".2", a1, nullptr, a2);
+        stw(p + ".1", a2, true);
+        stw(p + ".3", a2, false);
+        adaptor(p + ".4", a2);
+        temporal(p + ".5", a2, a2);
+      } else {
+        resblock(p + ".0", cur, nullptr, a1);
+        stw(p + ".1", a1, true);
+        resblock(p + ".2", a1, nullptr, a2);
+        stw(p + ".3", a2, false);
+        if (i > 1) adaptor(p + ".4", a2);
+      }
       skips.push_back(a2);
       if (i < nl - 1) {
         View dn = alloc_cf(B, dout, T, Hc / 2, Hc / 2);
-        conv(dn, a2, nullptr, P(p + ".5.weight"), 2, 1, D(p + ".5.bias"));
+        conv(dn, a2, nullptr, P(p + down_ix + ".weight"), 2, 1, D(p + down_ix + ".bias"));
         cur = dn;
         Hc /= 2;
       } else {
         cur = a2;
       }
     }
-    // mid (u12:1068-1072)
+    // mid (u12:1068-1072; ada_u22.py:1284-1288 orders b1, STW1, STW2, adaptor, b2)
     {
       const int md = dims[nl];
       View m1 = alloc_cf(B, md, T, Hc, Hc);
+      View m2 = alloc_cf(B, md, T, Hc, Hc);
       resblock("mid_block1", cur, nullptr, m1);
       stw("mid_attn1", m1, true);
-      View m2 = alloc_cf(B, md, T, Hc, Hc);
-      resblock("mid_block2", m1, nullptr, m2);
-      stw("mid_attn2", m2, false);
-      adaptor("mid_adaptor", m2);
+      if (u22) {
+        stw("mid_attn2", m1, false);
+        adaptor("mid_adaptor", m1);
+        resblock("mid_block2", m1, nullptr, m2);
+      } else {
+        resblock("mid_block2", m1, nullptr, m2);
+        stw("mid_attn2", m2, false);
+        adaptor("mid_adaptor", m2);
+      }
       cur = m2;
     }
-    // ups (u12:1074-1081)
+    // ups (u12:1074-1081; ada_u22.py:1291-1301)
     for (int i = 0; i < nl; ++i) {
       const std::string p = "ups." + std::to_string(i);
       const int din = dims[nl - 1 - i];
       View skip = skips.back();
       skips.pop_back();
       View u1 = alloc_cf(B, din, T, Hc, Hc);
-      resblock(p + ".0", cur, &skip, u1);
-      stw(p + ".1", u1, true);
       View u2 = alloc_cf(B, din, T, Hc, Hc);
-      resblock(p + ".2", u1, nullptr, u2);
-      stw(p + ".3", u2, false);
-      if (i > 1) adaptor(p + ".4", u2);
+      resblock(p + ".0", cur, &skip, u1);
+      if (u22) {
+        resblock(p + ".2", u1, nullptr, u2);
+        stw(p + ".1", u2, true);
+        stw(p + ".3", u2, false);
+        if (i > 1) adaptor(p + ".4", u2);
+        temporal(p + ".5", u2, u2);
+      } else {
+        stw(p + ".1", u1, true);
+        resblock(p + ".2", u1, nullptr, u2);
+        stw(p + ".3", u2, false);
+        if (i > 1) adaptor(p + ".4", u2);
+      }
       if (i < nl - 1) {
         View up = alloc_cf(B, din, T, Hc * 2, Hc * 2);
-        conv(up, u2, nullptr, Pdeconv(p + ".5.weight"), 1, 0, D(p + ".5.bias"));
+        conv(up, u2, nullptr, Pdeconv(p + down_ix + ".weight"), 1, 0, D(p + down_ix + ".bias"));
         cur = up;
         Hc *= 2;
       } else {
         cur = u2;
       }
     }
-    // heads (u12:1083-1086): final_conv -> flow (2), occlusion_map -> 1, frames tc:
+    // heads (u12:1083-1086): final_conv -> flow (2), occlusion_map -> 1, frames tm:
     {
       Scope sc(arena);
       View g = alloc_cf(B, d0, T, L, L);
@@ -740,16 +837,18 @@ struct ExtdmHandle {
       film = dmalloc((size_t)mtot * NT * sizeof(float));
       conv(cf_view(film, 1, mtot, 1, 1, NT), vte, nullptr, pw, 1, 0, dbias);
     }
-    // rotary tables (rotary-embedding-torch 0.8.3): angle = pos * freqs[i]
+    // rotary tables (rotary-embedding-torch 0.8.3): angle = pos * freqs[i], positions
+    // 0..63 (window tokens or frames), freqs of the first min(32, dim_head) dims
     {
       const HostTensor& fr = H("init_temporal_attn.fn.fn.fn.attn.rotary_emb.freqs");
-      REQUIRE(fr.f.size() == 16, "rotary freqs: dim_head 32 expected");
-      std::vector<float> c(32 * 16), sn(32 * 16);
-      for (int n = 0; n < 32; ++n)
-        for (int i = 0; i < 16; ++i) {
+      const int rh = cfg.dim_head / 2;
+      REQUIRE((int)fr.f.size() == rh, "rotary freqs: expected dim_head / 2 entries");
+      std::vector<float> c(64 * rh), sn(64 * rh);
+      for (int n = 0; n < 64; ++n)
+        for (int i = 0; i < rh; ++i) {
           const float a = (float)n * fr.f[i];
-          c[n * 16 + i] = std::cos(a);
-          sn[n * 16 + i] = std::sin(a);
+          c[n * rh + i] = std::cos(a);
+          sn[n * rh + i] = std::sin(a);
         }
       rope_cos = dmalloc(c.size() * 4);
       rope_sin = dmalloc(sn.size() * 4);
@@ -757,6 +856,8 @@ struct ExtdmHandle {
       HIPCHK(hipMemcpy(rope_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
     }
     // window relative-position bias, dense per layer: bias[h][i][j] = table[index[i][j]][h]
+    // ([heads][32][32] for windows of <= 32 tokens, [heads][64][64] for 4x4x4 windows).
+    // A window collapsed to a smaller extent uses index[:N', :N'] of the same table (u12:476).
     for (auto& kv : host) {
       const std::string& n = kv.first;
       const std::string suf = ".fn.fn.attn.relative_position_bias_table";
@@ -765,11 +866,13 @@ struct ExtdmHandle {
       const HostTensor& tab = kv.second;
       const HostTensor& idx = H(p + ".fn.fn.attn.relative_position_index");
       const int N = (int)idx.shape[0], nh = (int)tab.shape[1];
-      REQUIRE(N <= 32, "window larger than 32 tokens");
-      std::vector<float> d((size_t)nh * 1024, 0.f);
+      REQUIRE(N <= 64, "window larger than 64 tokens");
+      const int st = N <= 32 ? 32 : 64;
+      std::vector<float> d((size_t)nh * st * st, 0.f);
       for (int h = 0; h < nh; ++h)
         for (int i = 0; i < N; ++i)
-          for (int j = 0; j < N; ++j) d[(size_t)h * 1024 + i * 32 + j] = tab.f[(size_t)idx.i[(size_t)i * N + j] * nh + h];
+          for (int j = 0; j < N; ++j)
+            d[((size_t)h * st + i) * st + j] = tab.f[(size_t)idx.i[(size_t)i * N + j] * nh + h];
       float* dd = dmalloc(d.size() * 4);
       HIPCHK(hipMemcpy(dd, d.data(), d.size() * 4, hipMemcpyHostToDevice));
       bias_dense[p] = dd;
@@ -777,7 +880,7 @@ struct ExtdmHandle {
     // temporal T5 relative-position bias (RelativePositionBias, u12:42-79), max_distance 32
     {
       const HostTensor& emb = H("time_rel_pos_bias.relative_attention_bias.weight");
-      const int nh = (int)emb.shape[1], T = cfg.tc + cfg.tp;
+      const int nh = (int)emb.shape[1], T = frames();
       REQUIRE(T <= 32, "temporal attention over more than 32 frames");
       std::vector<float> d((size_t)nh * 1024, 0.f);
       const int nb = 16, max_exact = 8;
@@ -813,7 +916,9 @@ struct ExtdmHandle {
       finalize_workspace();
       return;
     }
-    REQUIRE(cfg.dim_head == 32, "this build supports attn_dim_head == 32");
+    REQUIRE(cfg.dim_head == 32 || cfg.dim_head == 16, "this build supports attn_dim_head 16 or 32");
+    REQUIRE(cfg.arch != EXTDM_ARCH_WO_REF || cfg.tc >= 2, "wo_ref needs at least two cond frames");
+    REQUIRE(frames() <= 32, "temporal attention over more than 32 frames");
     REQUIRE(cfg.heads % 4 == 0, "attn_heads must be a multiple of 4");
     // small tensors (biases, norm gains) go to the device now so that no
     // host->device copy can happen while a sampler step is being captured
@@ -925,7 +1030,7 @@ const char* extdm_last_error(void) { return g_last_error.c_str(); }
 int extdm_create(const ExtdmConfig* cfg, ExtdmHandle** out) {
   return guarded([&] {
     REQUIRE(cfg && out, "null argument");
-    REQUIRE(cfg->arch == EXTDM_ARCH_U12, "unsupported Unet3D architecture id");
+    REQUIRE(cfg->arch >= EXTDM_ARCH_U12 && cfg->arch <= EXTDM_ARCH_WO_REF, "unsupported Unet3D architecture id");
     REQUIRE(cfg->n_levels >= 1 && cfg->n_levels <= 4, "n_levels must be 1..4");
     int ndev = 0;
     HIPCHK(hipGetDeviceCount(&ndev));
@@ -1068,10 +1173,12 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     hipStream_t s = h->work;
     h->s = s;
     Scope sc(h->arena);
-    const int T = h->cfg.tc + h->cfg.tp, L = h->cfg.latent;
-    // layer 0: init_conv, conv3d (1,7,7) 512 -> dim over (B, T, L, L) (u12:913, 1041)
+    const int T = h->frames(), L = h->cfg.latent;
+    // layer 0: init_conv, conv3d (1,7,7) channels -> dim over (B, T, L, L) (u12:913, 1041),
+    // input as the forward issues it: two sources (x-branch, cond_fea branch)
     REQUIRE(layer == 0, "unknown layer id");
-    View x0 = h->alloc_cf(B, 256, T, L, L), fup = h->alloc_cf(B, h->cfg.channels - 256, T, L, L);
+    const int c1 = h->cfg.fea_ch, c0 = h->cfg.channels - c1;
+    View x0 = h->alloc_cf(B, c0, T, L, L), fup = h->alloc_cf(B, c1, T, L, L);
     View r = h->alloc_cf(B, h->cfg.dim, T, L, L);
     HIPCHK(hipMemsetAsync(x0.p, 0, x0.numel() * 4, s));
     HIPCHK(hipMemsetAsync(fup.p, 0, fup.numel() * 4, s));

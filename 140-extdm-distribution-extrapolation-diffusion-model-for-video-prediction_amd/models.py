@@ -1,6 +1,10 @@
 """Drop-in mirrors of the reference's sampling API, backed by the HIP library.
 
-  Unet3D             DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12.py:864-1086
+  Unet3D             DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12.py:864-1086 (== _u22)
+  Unet3DAda          DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_ada.py:865-1089
+  Unet3DAdaU22       DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_ada_u22.py:1009-1306
+  Unet3DWoRef        DenoiseNet_STWAtt_w_wo_ref_adaptor_cross_multi.py:755-967
+  UNET3D_BY_MODULE   reference module name -> class (what FlowDiffusion imports)
   GaussianDiffusion  model/BaseDM_adaptor/Diffusion.py:52-258
   Generator          model/LFAE/generator.py (decoder: forward_with_flow)
 
@@ -16,7 +20,8 @@ import torch
 from torch import nn
 
 from . import _lib
-from .spec import UnetConfig, unet_spec, GeneratorConfig, generator_spec, ARCH_U12
+from .spec import (UnetConfig, unet_spec, GeneratorConfig, generator_spec, ARCH_U12, ARCH_U22, ARCH_ADA,
+                   ARCH_ADA_U22, ARCH_WO_REF, ARCH_DEFAULTS)
 from .weights import synth_state_dict
 
 
@@ -46,13 +51,16 @@ def _register_tree(root, spec, init):
 
 class Unet3D(nn.Module):
     """Unet3D (u12). Same constructor surface as the reference; weights are
-    synthetic (seeded) until a checkpoint is loaded."""
+    synthetic (seeded) until a checkpoint is loaded. The variants below differ
+    only in their module's defaults and forward structure (spec.unet_spec,
+    runtime.cpp unet_forward)."""
+    ARCH = ARCH_U12
 
-    def __init__(self, dim, cond_dim=None, out_grid_dim=2, out_conf_dim=1, window_size=(2, 4, 4),
-                 dim_mults=(1, 2, 4), channels=3, cond_channels=3, attn_heads=8, attn_dim_head=32,
+    def __init__(self, dim, cond_dim=None, out_grid_dim=2, out_conf_dim=1, window_size=None,
+                 dim_mults=(1, 2, 4), channels=3, cond_channels=3, attn_heads=8, attn_dim_head=None,
                  use_bert_text_cond=False, init_dim=None, init_kernel_size=7, resnet_groups=8,
                  use_final_activation=False, learn_null_cond=False, use_deconv=True, padding_mode="zeros",
-                 cond_num=0, pred_num=0, framesize=32, seed=1234):
+                 cond_num=0, pred_num=0, framesize=32, l=None, seed=1234):
         super().__init__()
         if cond_dim is not None or use_bert_text_cond:
             raise NotImplementedError('text / vector conditioning is not on the ExtDM sampling path')
@@ -60,14 +68,21 @@ class Unet3D(nn.Module):
             raise NotImplementedError('only the reference FlowDiffusion construction of Unet3D is supported')
         if use_final_activation:
             raise NotImplementedError('use_final_activation=True is not used by any reference config')
+        if l is not None:
+            raise NotImplementedError('an explicit MotionAdaptor layer count (ada `l`) is not used by any config')
+        dwin, ddh = ARCH_DEFAULTS[self.ARCH]
+        window_size = dwin if window_size is None else window_size
+        attn_dim_head = ddh if attn_dim_head is None else attn_dim_head
         self.tc, self.tp = cond_num, pred_num
         self.channels = channels
         self.window_size = tuple(window_size)
         self.has_cond = False
         self.null_cond_mask = None
+        # cond_fea arrives at the LFAE bottleneck size, or at flow size for wo_ref (multi1248.py:243-245)
+        fea_size = framesize if self.ARCH == ARCH_WO_REF else framesize // 2
         self.ucfg = UnetConfig(dim=dim, channels=channels, dim_mults=tuple(dim_mults), window=tuple(window_size),
                                heads=attn_heads, dim_head=attn_dim_head, tc=cond_num, tp=pred_num, latent=framesize,
-                               fea_size=framesize // 2, arch=ARCH_U12)
+                               fea_size=fea_size, arch=self.ARCH)
         spec = unet_spec(self.ucfg)
         _register_tree(self, spec, synth_state_dict(spec, seed=seed, window=self.window_size))
         self._native = None
@@ -110,7 +125,7 @@ class Unet3D(nn.Module):
         tc, tp = cond_frames.shape[2], x.shape[2]
         assert tc == self.tc
         assert tp == self.tp
-        assert cond_fea.shape[2] == tc + tp
+        assert cond_fea.shape[2] == self.ucfg.frames
         if not x.is_cuda:
             raise RuntimeError('ExtDM HIP path needs tensors on a ROCm device (no CPU fallback)')
         B = x.shape[0]
@@ -120,6 +135,35 @@ class Unet3D(nn.Module):
         h.unet_forward(x.float().contiguous(), t, cond_frames.float().contiguous(), cond_fea.float().contiguous(),
                        out)
         return out
+
+
+class Unet3DAda(Unet3D):
+    """KTH denoiser: 4x4x4 windows, dim_head 16, cond_adaptor + cond_temporal_attn on
+    cond_fea instead of TrajWarp (ada.py:918-920, 1034-1036)."""
+    ARCH = ARCH_ADA
+
+
+class Unet3DAdaU22(Unet3D):
+    """Cityscapes / UCF denoiser: no init_noise_conv in forward, per-level order
+    b1, b2, STW, STW, adaptor, temporal attention (ada_u22.py:1172-1306)."""
+    ARCH = ARCH_ADA_U22
+
+    def forward(self, x, time, cond_frames, cond_fea=None, cond=None, null_cond_prob=0., none_cond_mask=None,
+                path=0):
+        if path != 0:
+            # path=1 hard-codes T=30 and is never passed by the CLI (SURVEY §8 a20)
+            raise NotImplementedError('ada_u22 path=1 (combined THW bias) is not on the sampling path')
+        return super().forward(x, time, cond_frames, cond_fea, cond, null_cond_prob, none_cond_mask)
+
+
+class Unet3DWoRef(Unet3D):
+    """SMMNIST denoiser: cond_frames[:, :, :-1], cond_fea at flow resolution with
+    tc-1+tp frames, MotionAdaptor tm = tc-1 (wo_ref.py:906-967)."""
+    ARCH = ARCH_WO_REF
+
+
+UNET3D_BY_MODULE = {ARCH_U12: Unet3D, ARCH_U22: Unet3D, ARCH_ADA: Unet3DAda, ARCH_ADA_U22: Unet3DAdaU22,
+                    ARCH_WO_REF: Unet3DWoRef}
 
 
 def schedule_buffers(timesteps, s=0.008):

@@ -1,10 +1,12 @@
 """Model configuration and state_dict layout of the ExtDM sampling path.
 
 `unet_spec(cfg)` lists the Unet3D state_dict entries (name, shape, dtype) in the
-exact order the reference registers them
-(model/BaseDM_adaptor/DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12.py:864-1003),
-so reference DM checkpoints (`checkpoint['diffusion']`, keys `denoise_fn.*`)
-load strict-compatible and synthetic weights are generated in reference order.
+exact order the reference registers them, for each of the four denoisers
+(model/BaseDM_adaptor/DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12.py:864-1003,
+..._traj_ada.py:865-1018, ..._traj_ada_u22.py:1009-1170,
+DenoiseNet_STWAtt_w_wo_ref_adaptor_cross_multi.py:755-904), so reference DM
+checkpoints (`checkpoint['diffusion']`, keys `denoise_fn.*`) load
+strict-compatible and synthetic weights are generated in reference order.
 `generator_spec(gcfg)` does the same for the LFAE Generator decoder
 (model/LFAE/generator.py:26-62, util.py:69-149).
 """
@@ -13,13 +15,23 @@ from dataclasses import dataclass, field
 
 ARCH_U12 = 'DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12'
 ARCH_U22 = 'DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u22'  # byte-identical to u12
-ARCH_IDS = {ARCH_U12: 0, ARCH_U22: 0}
+ARCH_ADA = 'DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_ada'
+ARCH_ADA_U22 = 'DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_ada_u22'
+ARCH_WO_REF = 'DenoiseNet_STWAtt_w_wo_ref_adaptor_cross_multi'
+# ids of include/extdm.h EXTDM_ARCH_*
+ARCH_IDS = {ARCH_U12: 0, ARCH_U22: 0, ARCH_ADA: 1, ARCH_ADA_U22: 2, ARCH_WO_REF: 3}
+ARCH_SHORT = {ARCH_U12: 'u12', ARCH_U22: 'u12', ARCH_ADA: 'ada', ARCH_ADA_U22: 'ada_u22', ARCH_WO_REF: 'wo_ref'}
+# constructor defaults that differ per module (window_size, attn_dim_head)
+ARCH_DEFAULTS = {ARCH_U12: ((2, 4, 4), 32), ARCH_U22: ((2, 4, 4), 32), ARCH_ADA: ((4, 4, 4), 16),
+                 ARCH_ADA_U22: ((4, 4, 4), 32), ARCH_WO_REF: ((2, 4, 4), 32)}
 
 
 @dataclass
 class UnetConfig:
     """Constructor surface of Unet3D as FlowDiffusion builds it
-    (VideoFlowDiffusion_multi_w_ref.py:80-94)."""
+    (VideoFlowDiffusion_multi_w_ref.py:80-94; _u22.py:199-213; multi1248.py:70-84).
+    `fea_size` is the cond_fea H = W: the LFAE bottleneck (latent / 2) for the
+    feature-branch denoisers, the latent itself for wo_ref (multi1248.py:243-245)."""
     dim: int = 64
     channels: int = 512
     dim_mults: tuple = (1, 2, 4, 4)
@@ -29,9 +41,36 @@ class UnetConfig:
     tc: int = 2
     tp: int = 14
     latent: int = 32           # flow / latent H = W
-    fea_size: int = 16         # cond_fea spatial size (LFAE bottleneck)
+    fea_size: int = 16         # cond_fea spatial size
     fea_ch: int = 256
     arch: str = ARCH_U12
+
+    @classmethod
+    def for_arch(cls, arch, **kw):
+        """Defaults of the named reference module, then overrides."""
+        win, dh = ARCH_DEFAULTS[arch]
+        base = dict(window=win, dim_head=dh, arch=arch)
+        if arch in (ARCH_ADA_U22, ARCH_WO_REF):
+            base['channels'] = 3 + 256
+        if arch == ARCH_WO_REF:
+            base['dim_mults'] = (1, 2, 4, 8)
+        base.update(kw)
+        if arch == ARCH_WO_REF and 'fea_size' not in kw:
+            base['fea_size'] = base.get('latent', 32)
+        return cls(**base)
+
+    @property
+    def short(self):
+        return ARCH_SHORT[self.arch]
+
+    @property
+    def tm(self):
+        """cond frames the denoiser sees (wo_ref drops the last: wo_ref.py:911)."""
+        return self.tc - 1 if self.arch == ARCH_WO_REF else self.tc
+
+    @property
+    def frames(self):
+        return self.tm + self.tp
 
     def levels(self):
         dims = [self.dim] + [self.dim * m for m in self.dim_mults]
@@ -39,7 +78,8 @@ class UnetConfig:
 
     def as_dict(self):
         return {'dim': self.dim, 'dim_mults': tuple(self.dim_mults), 'window': tuple(self.window),
-                'heads': self.heads, 'dim_head': self.dim_head, 'tc': self.tc, 'tp': self.tp}
+                'heads': self.heads, 'dim_head': self.dim_head, 'tc': self.tc, 'tp': self.tp,
+                'arch': self.short}
 
 
 def adaptor_layers(tm, tp):
@@ -73,49 +113,70 @@ def _stw(out, p, d, cfg):
 
 
 def _adaptor(out, p, d, cfg):
-    L, Fr = adaptor_layers(cfg.tc, cfg.tp)
+    L, Fr = adaptor_layers(cfg.tm, cfg.tp)
     ap = f'{p}.adaptors'
     out += [(f'{ap}.predictor.fn.fn.weight', (d, d, 1, 1, 1)), (f'{ap}.predictor.fn.fn.bias', (d,)),
             (f'{ap}.predictor.fn.norm.gamma', (1, d, 1, 1, 1))]
+    kt = 3 if cfg.short == 'ada_u22' else 1  # ada_u22 extrapolates with full 3x3x3 convs (ada_u22.py:537)
     for l in range(L):
-        out += [(f'{ap}.extrapolators.{l}.fn.weight', (d, d, 1, 3, 3))]
+        out += [(f'{ap}.extrapolators.{l}.fn.weight', (d, d, kt, 3, 3))]
     out += [(f'{p}.Tmodulator.weight', (d * cfg.tp, d * Fr, 1, 1)), (f'{p}.Tmodulator.bias', (d * cfg.tp,)),
             (f'{p}.fuser.fn.weight', (d, 2 * d, 1, 1, 1)), (f'{p}.fuser.fn.bias', (d,)),
             (f'{p}.fuser.norm.gamma', (1, 2 * d, 1, 1, 1))]
 
 
-def unet_spec(cfg: UnetConfig):
-    """Ordered (name, shape, dtype) list of the u12 Unet3D state_dict."""
-    out = []
+def _temporal(out, p, d, cfg):
+    """Residual(PreNorm(d, EinopsToAndFrom(AttentionLayer))) (u12:903-915)."""
     hid = cfg.heads * cfg.dim_head
+    a = f'{p}.fn.fn.fn'
+    out += [(f'{a}.norm.weight', (d,)), (f'{a}.norm.bias', (d,)),
+            (f'{a}.attn.rotary_emb.freqs', (min(32, cfg.dim_head) // 2,)),
+            (f'{a}.attn.to_qkv.weight', (3 * hid, d)), (f'{a}.attn.to_out.weight', (d, hid)),
+            (f'{p}.fn.norm.gamma', (1, d, 1, 1, 1))]
+
+
+def unet_spec(cfg: UnetConfig):
+    """Ordered (name, shape, dtype) list of the Unet3D state_dict of cfg.arch."""
+    arch = cfg.short
+    u22 = arch == 'ada_u22'
+    out = []
     d0 = cfg.dim
     tdim = cfg.dim * 4
-    out += [('time_rel_pos_bias.relative_attention_bias.weight', (32, cfg.heads)),
-            ('init_conv.weight', (d0, cfg.channels, 1, 7, 7)), ('init_conv.bias', (d0,)),
-            ('init_noise_conv.weight', (256, 3, 1, 7, 7)), ('init_noise_conv.bias', (256,))]
-    a = 'init_temporal_attn.fn.fn.fn'
-    out += [(f'{a}.norm.weight', (d0,)), (f'{a}.norm.bias', (d0,)),
-            (f'{a}.attn.rotary_emb.freqs', (min(32, cfg.dim_head) // 2,)),
-            (f'{a}.attn.to_qkv.weight', (3 * hid, d0)), (f'{a}.attn.to_out.weight', (d0, hid)),
-            ('init_temporal_attn.fn.norm.gamma', (1, d0, 1, 1, 1))]
-    _adaptor(out, 'init_adaptor', 256, cfg)
-    for n in ('q', 'k', 'v', 'o'):
-        out += [(f'init_traj.cross_att.linear_{n}.weight', (256, 256)),
-                (f'init_traj.cross_att.linear_{n}.bias', (256,))]
-    out += [('init_traj.fuser.weight', (256, 512, 1, 1, 1)), ('init_traj.fuser.bias', (256,)),
-            ('time_mlp.1.weight', (tdim, cfg.dim)), ('time_mlp.1.bias', (tdim,)),
+    if u22:  # direct Parameters come first in state_dict order (ada_u22.py:1120-1121)
+        out += [('alpha', (cfg.heads,)), ('beta', (cfg.heads,))]
+    out += [('time_rel_pos_bias.relative_attention_bias.weight', (32, cfg.heads))]
+    if u22:
+        out += [('rel_pos_bias_thw.relative_attention_bias.weight', (32, cfg.heads))]
+    out += [('init_conv.weight', (d0, cfg.channels, 1, 7, 7)), ('init_conv.bias', (d0,))]
+    if arch != 'wo_ref':
+        out += [('init_noise_conv.weight', (256, 3, 1, 7, 7)), ('init_noise_conv.bias', (256,))]
+    _temporal(out, 'init_temporal_attn', d0, cfg)
+    if arch == 'u12':
+        _adaptor(out, 'init_adaptor', 256, cfg)
+        for n in ('q', 'k', 'v', 'o'):
+            out += [(f'init_traj.cross_att.linear_{n}.weight', (256, 256)),
+                    (f'init_traj.cross_att.linear_{n}.bias', (256,))]
+        out += [('init_traj.fuser.weight', (256, 512, 1, 1, 1)), ('init_traj.fuser.bias', (256,))]
+    elif arch in ('ada', 'ada_u22'):
+        _temporal(out, 'cond_temporal_attn', 256, cfg)
+        _adaptor(out, 'cond_adaptor', 256, cfg)
+    out += [('time_mlp.1.weight', (tdim, cfg.dim)), ('time_mlp.1.bias', (tdim,)),
             ('time_mlp.3.weight', (tdim, tdim)), ('time_mlp.3.bias', (tdim,))]
     lv = cfg.levels()
+    samp = '6' if u22 else '5'
     for i, (din, dout) in enumerate(lv):
         p = f'downs.{i}'
         _resnet(out, p + '.0', din, dout, tdim)
         _stw(out, p + '.1', dout, cfg)
         _resnet(out, p + '.2', dout, dout, tdim)
         _stw(out, p + '.3', dout, cfg)
-        if i > 1:
+        if i > 1 or u22:
             _adaptor(out, p + '.4', dout, cfg)
+        if u22:
+            _temporal(out, p + '.5', dout, cfg)
         if i < len(lv) - 1:
-            out += [(f'{p}.5.weight', (dout, dout, 1, 4, 4)), (f'{p}.5.bias', (dout,))]
+            out += [(f'{p}.{samp}.weight', (dout, dout, 1, 4, 4)), (f'{p}.{samp}.bias', (dout,))]
+    # the `ups` ModuleList is registered before mid_block1 (u12:946-947)
     for i, (din, dout) in enumerate(reversed(lv)):
         p = f'ups.{i}'
         _resnet(out, p + '.0', dout * 2, din, tdim)
@@ -124,9 +185,10 @@ def unet_spec(cfg: UnetConfig):
         _stw(out, p + '.3', din, cfg)
         if i > 1:
             _adaptor(out, p + '.4', din, cfg)
+        if u22:
+            _temporal(out, p + '.5', din, cfg)
         if i < len(lv) - 1:
-            out += [(f'{p}.5.weight', (din, din, 1, 4, 4)), (f'{p}.5.bias', (din,))]
-    # the `ups` ModuleList is registered before mid_block1 (u12:946-947)
+            out += [(f'{p}.{samp}.weight', (din, din, 1, 4, 4)), (f'{p}.{samp}.bias', (din,))]
     md = lv[-1][1]
     _resnet(out, 'mid_block1', md, md, tdim)
     _stw(out, 'mid_attn1', md, cfg)

@@ -61,7 +61,7 @@ def synth_state_dict(spec, seed=1234, window=(2, 4, 4)):
             v = 0.1 * z
         else:
             fan_in = int(np.prod(shape[1:]))
-            if '.5.weight' in name and name.startswith('ups.'):
+            if name.startswith('ups.') and len(shape) == 5 and tuple(shape[2:]) == (1, 4, 4):
                 # ConvTranspose3d weight is (Cin, Cout, kt, kh, kw): fan-in = Cin*k*k/4
                 fan_in = shape[0] * shape[2] * shape[3] * shape[4] // 4
             v = z / math.sqrt(fan_in)

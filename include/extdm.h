@@ -10,11 +10,14 @@
  *
  * Reference interfaces replaced (file:line in the reference tree):
  *   extdm_create / extdm_load_weight / extdm_finalize
- *       Unet3D.__init__ + load_state_dict          DenoiseNet_..._u12.py:864-1003
+ *       Unet3D.__init__ + load_state_dict          DenoiseNet_..._u12.py:864-1003,
+ *                                                   _ada.py:865-1018, _ada_u22.py:1009-1170,
+ *                                                   _wo_ref_adaptor_cross_multi.py:755-904
  *       GaussianDiffusion.__init__ buffers          Diffusion.py:52-122
  *       Generator.__init__ (decoder half)           LFAE/generator.py:26-62
  *   extdm_unet_forward   Unet3D.forward / forward_with_cond_scale(cond_scale=1)
- *                                                   u12:1005-1086
+ *                                                   u12:1005-1086, ada:1020-1089,
+ *                                                   ada_u22:1172-1306 (path=0), wo_ref:906-967
  *   extdm_sample         GaussianDiffusion.p_sample_loop / ddim_sample
  *                                                   Diffusion.py:180-189, 209-258
  *   extdm_sampler_step   one p_sample / DDIM update given eps
@@ -33,11 +36,17 @@ extern "C" {
 
 typedef struct ExtdmHandle ExtdmHandle;
 
-enum { EXTDM_ARCH_U12 = 0 };
+/* Unet3D denoiser variants, one per reference module:
+ *   U12      DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12.py (== _u22.py): BAIR
+ *   ADA      ..._traj_ada.py: KTH (window 4x4x4, dim_head 16, cond_adaptor + cond_temporal_attn)
+ *   ADA_U22  ..._traj_ada_u22.py: Cityscapes / UCF (b1,b2,STW,STW,adaptor,temporal per level)
+ *   WO_REF   DenoiseNet_STWAtt_w_wo_ref_adaptor_cross_multi.py: SMMNIST (tc-1 cond frames,
+ *            cond_fea at latent resolution, fea: [B,fea_ch,tc-1+tp,L,L]) */
+enum { EXTDM_ARCH_U12 = 0, EXTDM_ARCH_ADA = 1, EXTDM_ARCH_ADA_U22 = 2, EXTDM_ARCH_WO_REF = 3 };
 enum { EXTDM_SAMPLER_DDPM = 0, EXTDM_SAMPLER_DDIM = 1 };
 
 typedef struct ExtdmConfig {
-  int arch;            /* EXTDM_ARCH_* (u12 == u22) */
+  int arch;            /* EXTDM_ARCH_* */
   int dim;             /* Unet base width (64) */
   int channels;        /* init_conv input channels (256 + 256) */
   int dim_mults[4];
@@ -71,7 +80,8 @@ int extdm_finalize(ExtdmHandle* h);
 int64_t extdm_workspace_bytes(const ExtdmHandle* h);
 
 /* eps = Unet3D(x, t, cond_frames, cond_fea). x, out: [B,3,tp,L,L]; t: int64 [B];
- * cond: [B,3,tc,L,L]; fea: [B,fea_ch,tc+tp,fs,fs]. All device pointers. */
+ * cond: [B,3,tc,L,L]; fea: [B,fea_ch,T,fs,fs] with T = tc+tp (tc-1+tp for WO_REF).
+ * All device pointers. */
 int extdm_unet_forward(ExtdmHandle* h, int B, const float* x, const int64_t* t, const float* cond,
                        const float* fea, float* out, void* stream);
 

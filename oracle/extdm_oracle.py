@@ -374,7 +374,9 @@ def motion_adaptor(sd, p, x, tc, tp):
         std = (flat.var(dim=2) + 1e-5).sqrt().view(N, C, 1, 1, 1)
         mean = flat.mean(dim=2).view(N, C, 1, 1, 1)
         h = (cur - mean) / std
-        h = F.conv3d(h, sd[f'{ap}.extrapolators.{l}.fn.weight'], None, padding=(0, 1, 1)) + h
+        wx = sd[f'{ap}.extrapolators.{l}.fn.weight']
+        # (1,3,3) zero-init in u12/ada/wo_ref; a full 3x3x3 conv in ada_u22 (ada_u22.py:537)
+        h = F.conv3d(h, wx, None, padding=(wx.shape[2] // 2, 1, 1)) + h
         cur = torch.cat([cur, h * std + mean], dim=2)
     ext = cur[:, :, tc:]
     N, C, Tf, H, W = ext.shape
@@ -421,61 +423,112 @@ def unet_levels(cfg):
     return list(zip(dims[:-1], dims[1:]))
 
 
+def _resize_frames(f, size):
+    """rearrange '(n t) c h w' + F.interpolate(bilinear, align_corners=False) (u12:1035-1037)."""
+    n, c, T = f.shape[:3]
+    f = f.permute(0, 2, 1, 3, 4).reshape(n * T, c, *f.shape[3:])
+    f = F.interpolate(f, size=size, mode='bilinear')
+    return f.reshape(n, T, c, *size).permute(0, 2, 1, 3, 4)
+
+
 def unet_forward(sd, cfg, x, time, cond_frames, cond_fea):
-    """Unet3D.forward for the u12 architecture (u12:1017-1086)."""
+    """Unet3D.forward for the four reference denoisers, cfg['arch'] in
+    u12      DenoiseNet_..._traj_u12.py:1017-1086 (== u22)
+    ada      DenoiseNet_..._traj_ada.py:1020-1089  (cond_adaptor + cond_temporal_attn)
+    ada_u22  DenoiseNet_..._traj_ada_u22.py:1172-1306 (path=0; no init_noise_conv,
+             b1, b2, STW, STW, adaptor, temporal attention per level)
+    wo_ref   DenoiseNet_STWAtt_w_wo_ref_adaptor_cross_multi.py:906-967 (drops the last
+             cond frame, cond_fea at latent resolution, adaptor tm = tc-1)."""
+    arch = cfg.get('arch', 'u12')
     tc, tp = cfg['tc'], cfg['tp']
     heads, dh = cfg['heads'], cfg['dim_head']
     win = tuple(cfg['window'])
     shift = tuple(w // 2 for w in win)
-    assert cond_frames.shape[2] == tc and x.shape[2] == tp and cond_fea.shape[2] == tc + tp
-    x = torch.cat([cond_frames, x], dim=2)
-    pb = time_pos_bias(sd, tc + tp)
-    x = F.conv3d(x, sd['init_noise_conv.weight'], sd['init_noise_conv.bias'], padding=(0, 3, 3))
-    f = traj_warp(sd, 'init_traj', x[:, :, tc:], cond_fea, tc, tp, heads)
-    n, c, T = f.shape[:3]
-    f = f.permute(0, 2, 1, 3, 4).reshape(n * T, c, *f.shape[3:])
-    f = F.interpolate(f, size=x.shape[-2:], mode='bilinear')
-    f = f.reshape(n, T, c, *x.shape[-2:]).permute(0, 2, 1, 3, 4)
-    x = torch.cat([x, f], dim=1)
+    u22 = arch == 'ada_u22'
+    assert cond_frames.shape[2] == tc and x.shape[2] == tp
+    if arch == 'wo_ref':
+        tm = tc - 1
+        x = torch.cat([cond_frames[:, :, :-1], x], dim=2)
+    else:
+        tm = tc
+        x = torch.cat([cond_frames, x], dim=2)
+    assert cond_fea.shape[2] == tm + tp
+    pb = time_pos_bias(sd, tm + tp)
+    if arch == 'wo_ref':
+        x = torch.cat([x, cond_fea], dim=1)
+    else:
+        if arch != 'ada_u22':
+            x = F.conv3d(x, sd['init_noise_conv.weight'], sd['init_noise_conv.bias'], padding=(0, 3, 3))
+        if arch == 'u12':
+            f = traj_warp(sd, 'init_traj', x[:, :, tc:], cond_fea, tc, tp, heads)
+        else:
+            f = motion_adaptor(sd, 'cond_adaptor', cond_fea, tm, tp)
+            f = temporal_attention(sd, 'cond_temporal_attn', f, pb, heads, dh)
+        x = torch.cat([x, _resize_frames(f, x.shape[-2:])], dim=1)
     x = F.conv3d(x, sd['init_conv.weight'], sd['init_conv.bias'], padding=(0, 3, 3))
     r = x.clone()
     x = temporal_attention(sd, 'init_temporal_attn', x, pb, heads, dh)
     t = time_mlp(sd, time, cfg['dim'])
     levels = unet_levels(cfg)
+    nl = len(levels)
+    sample_ix = '.6' if u22 else '.5'
     skips = []
-    for i in range(len(levels)):
+    for i in range(nl):
         p = f'downs.{i}'
-        x = resnet_block(sd, p + '.0', x, t)
-        x = stw_attention(sd, p + '.1', x, win, shift, heads, dh)
-        x = resnet_block(sd, p + '.2', x, t)
-        x = stw_attention(sd, p + '.3', x, win, (0, 0, 0), heads, dh)
-        if i > 1:
-            x = motion_adaptor(sd, p + '.4', x, tc, tp)
+        if u22:
+            x = resnet_block(sd, p + '.0', x, t)
+            x = resnet_block(sd, p + '.2', x, t)
+            x = stw_attention(sd, p + '.1', x, win, shift, heads, dh)
+            x = stw_attention(sd, p + '.3', x, win, (0, 0, 0), heads, dh)
+            x = motion_adaptor(sd, p + '.4', x, tm, tp)
+            x = temporal_attention(sd, p + '.5', x, pb, heads, dh)
+        else:
+            x = resnet_block(sd, p + '.0', x, t)
+            x = stw_attention(sd, p + '.1', x, win, shift, heads, dh)
+            x = resnet_block(sd, p + '.2', x, t)
+            x = stw_attention(sd, p + '.3', x, win, (0, 0, 0), heads, dh)
+            if i > 1:
+                x = motion_adaptor(sd, p + '.4', x, tm, tp)
         skips.append(x)
-        if i < len(levels) - 1:
-            x = F.conv3d(x, sd[p + '.5.weight'], sd[p + '.5.bias'], stride=(1, 2, 2), padding=(0, 1, 1))
+        if i < nl - 1:
+            x = F.conv3d(x, sd[p + sample_ix + '.weight'], sd[p + sample_ix + '.bias'], stride=(1, 2, 2),
+                         padding=(0, 1, 1))
     x = resnet_block(sd, 'mid_block1', x, t)
     x = stw_attention(sd, 'mid_attn1', x, win, shift, heads, dh)
-    x = resnet_block(sd, 'mid_block2', x, t)
-    x = stw_attention(sd, 'mid_attn2', x, win, (0, 0, 0), heads, dh)
-    x = motion_adaptor(sd, 'mid_adaptor', x, tc, tp)
-    for i in range(len(levels)):
+    if u22:
+        x = stw_attention(sd, 'mid_attn2', x, win, (0, 0, 0), heads, dh)
+        x = motion_adaptor(sd, 'mid_adaptor', x, tm, tp)
+        x = resnet_block(sd, 'mid_block2', x, t)
+    else:
+        x = resnet_block(sd, 'mid_block2', x, t)
+        x = stw_attention(sd, 'mid_attn2', x, win, (0, 0, 0), heads, dh)
+        x = motion_adaptor(sd, 'mid_adaptor', x, tm, tp)
+    for i in range(nl):
         p = f'ups.{i}'
         x = torch.cat((x, skips.pop()), dim=1)
-        x = resnet_block(sd, p + '.0', x, t)
-        x = stw_attention(sd, p + '.1', x, win, shift, heads, dh)
-        x = resnet_block(sd, p + '.2', x, t)
-        x = stw_attention(sd, p + '.3', x, win, (0, 0, 0), heads, dh)
-        if i > 1:
-            x = motion_adaptor(sd, p + '.4', x, tc, tp)
-        if i < len(levels) - 1:
-            x = F.conv_transpose3d(x, sd[p + '.5.weight'], sd[p + '.5.bias'], stride=(1, 2, 2),
-                                   padding=(0, 1, 1))
+        if u22:
+            x = resnet_block(sd, p + '.0', x, t)
+            x = resnet_block(sd, p + '.2', x, t)
+            x = stw_attention(sd, p + '.1', x, win, shift, heads, dh)
+            x = stw_attention(sd, p + '.3', x, win, (0, 0, 0), heads, dh)
+            if i > 1:
+                x = motion_adaptor(sd, p + '.4', x, tm, tp)
+            x = temporal_attention(sd, p + '.5', x, pb, heads, dh)
+        else:
+            x = resnet_block(sd, p + '.0', x, t)
+            x = stw_attention(sd, p + '.1', x, win, shift, heads, dh)
+            x = resnet_block(sd, p + '.2', x, t)
+            x = stw_attention(sd, p + '.3', x, win, (0, 0, 0), heads, dh)
+            if i > 1:
+                x = motion_adaptor(sd, p + '.4', x, tm, tp)
+        if i < nl - 1:
+            x = F.conv_transpose3d(x, sd[p + sample_ix + '.weight'], sd[p + sample_ix + '.bias'],
+                                   stride=(1, 2, 2), padding=(0, 1, 1))
     x = torch.cat((x, r), dim=1)
     g = resnet_block(sd, 'final_conv.0', x)
-    g = F.conv3d(g, sd['final_conv.1.weight'], sd['final_conv.1.bias'])[:, :, tc:]
+    g = F.conv3d(g, sd['final_conv.1.weight'], sd['final_conv.1.bias'])[:, :, tm:]
     o = resnet_block(sd, 'occlusion_map.0', x)
-    o = F.conv3d(o, sd['occlusion_map.1.weight'], sd['occlusion_map.1.bias'])[:, :, tc:]
+    o = F.conv3d(o, sd['occlusion_map.1.weight'], sd['occlusion_map.1.bias'])[:, :, tm:]
     return torch.cat((g, o), dim=1)
 
 

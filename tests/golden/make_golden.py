@@ -21,7 +21,8 @@ REPO = os.path.dirname(os.path.dirname(HERE))
 REF = '/root/reference'
 
 sys.path.insert(0, REPO)
-from tests.golden_inputs import CONFIGS, GEN_CFG, unet_inputs, decoder_inputs, make_sd, make_gen_sd, PKG  # noqa: E402
+from tests.golden_inputs import (CONFIGS, GEN_CFG, VARIANTS, GOLDEN_BATCH, unet_inputs, decoder_inputs,  # noqa: E402
+                                 make_sd, make_gen_sd, PKG)
 
 spec = importlib.import_module(PKG + '.spec')
 
@@ -35,6 +36,30 @@ def import_reference():
     from model.BaseDM_adaptor.Diffusion import GaussianDiffusion
     from model.LFAE.generator import Generator
     return Unet3D, GaussianDiffusion, Generator
+
+
+REF_MODULES = {'ada': 'DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_ada',
+               'ada_u22': 'DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_ada_u22',
+               'wo_ref': 'DenoiseNet_STWAtt_w_wo_ref_adaptor_cross_multi'}
+
+
+def variants():
+    """One forward per denoiser variant: keys + eps."""
+    keys = json.load(open(os.path.join(HERE, 'unet_keys.json')))
+    for name in VARIANTS:
+        cfg = CONFIGS[name]
+        mod = importlib.import_module('model.BaseDM_adaptor.' + REF_MODULES[cfg.short])
+        net = build_ref_unet(mod.Unet3D, cfg)
+        ref_sd = net.state_dict()
+        keys[name] = [[k, list(v.shape), str(v.dtype).replace('torch.', '')] for k, v in ref_sd.items()]
+        net.load_state_dict(make_sd(cfg), strict=True)
+        x, t, cond, fea = unet_inputs(cfg, B=GOLDEN_BATCH.get(name, 2))
+        with torch.no_grad():
+            eps = net(x, t, cond, cond_fea=fea)
+        np.savez_compressed(os.path.join(HERE, f'unet_{name}.npz'), eps=eps.numpy())
+        print(name, 'eps', tuple(eps.shape), float(eps.abs().mean()))
+    with open(os.path.join(HERE, 'unet_keys.json'), 'w') as f:
+        json.dump(keys, f)
 
 
 def build_ref_unet(Unet3D, cfg):
@@ -162,4 +187,10 @@ def main():
 
 
 if __name__ == '__main__':
-    main()
+    if '--variants' in sys.argv:
+        torch.set_num_threads(8)
+        import_reference()
+        variants()
+    else:
+        main()
+        variants()

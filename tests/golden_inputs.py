@@ -14,12 +14,25 @@ PKG = '140-extdm-distribution-extrapolation-diffusion-model-for-video-prediction
 _spec = importlib.import_module(PKG + '.spec')
 _w = importlib.import_module(PKG + '.weights')
 
+_for = _spec.UnetConfig.for_arch
 CONFIGS = {
-    # reduced: dim 16, tp 6, 16x16 latent (exercises the 2x2 window collapse)
+    # u12: reduced (dim 16, tp 6, 16x16 latent: exercises the 2x2 window collapse)
     'small': _spec.UnetConfig(dim=16, tc=2, tp=6, latent=16, fea_size=8),
-    # BAIR 64x64 2->14 per round (BASELINE configs[1])
+    # u12: BAIR 64x64 2->14 per round (BASELINE configs[1])
     'bair': _spec.UnetConfig(),
+    # ada (KTH module): 4x4x4 windows, dim_head 16; reduced, and the KTH 10->20 round
+    'ada_small': _for(_spec.ARCH_ADA, tc=2, tp=6, latent=16, fea_size=8),
+    'ada_kth': _for(_spec.ARCH_ADA, tc=10, tp=20),
+    # ada_u22 (Cityscapes module): T = 7 pads to 8 in 4x4x4 windows
+    'u22_small': _for(_spec.ARCH_ADA_U22, tc=2, tp=5, latent=16, fea_size=8),
+    'u22_city': _for(_spec.ARCH_ADA_U22, tc=2, tp=5),
+    # wo_ref (SMMNIST module): dims (1,2,4,8), tc-1 cond frames, cond_fea at latent size
+    'woref_small': _for(_spec.ARCH_WO_REF, tc=3, tp=4, latent=16),
+    'woref_smmnist': _for(_spec.ARCH_WO_REF, tc=10, tp=5),
 }
+VARIANTS = ['ada_small', 'ada_kth', 'u22_small', 'u22_city', 'woref_small', 'woref_smmnist']
+# the batch each golden forward is run at
+GOLDEN_BATCH = {'ada_kth': 1, 'u22_city': 1, 'woref_smmnist': 1}
 GEN_CFG = _spec.GeneratorConfig()
 
 
@@ -36,7 +49,7 @@ def unet_inputs(cfg, B=2, seed=99):
     L, fs = cfg.latent, cfg.fea_size
     x = torch.from_numpy(rng.standard_normal((B, 3, cfg.tp, L, L), dtype=np.float32))
     cond = torch.from_numpy((rng.random((B, 3, cfg.tc, L, L), dtype=np.float32) * 2 - 1))
-    fea = torch.from_numpy(rng.standard_normal((B, cfg.fea_ch, cfg.tc + cfg.tp, fs, fs), dtype=np.float32))
+    fea = torch.from_numpy(rng.standard_normal((B, cfg.fea_ch, cfg.frames, fs, fs), dtype=np.float32))
     t = torch.tensor([999, 1] + [500] * (B - 2), dtype=torch.long)[:B]
     return x, t, cond, fea
 

@@ -14,7 +14,8 @@ import numpy as np
 import pytest
 import torch
 
-from tests.golden_inputs import CONFIGS, PKG, make_sd, unet_inputs, make_gen_sd, decoder_inputs, GEN_CFG
+from tests.golden_inputs import (CONFIGS, PKG, VARIANTS, GOLDEN_BATCH, make_sd, unet_inputs, make_gen_sd,
+                                 decoder_inputs, GEN_CFG)
 from tests.test_oracle_golden import load
 
 pytestmark = pytest.mark.gpu
@@ -57,6 +58,44 @@ def test_unet_forward_vs_reference_golden(name):
     g = load(f'unet_{name}.npz')['eps']
     err = np.abs(eps.numpy() - g).max()
     assert err <= 1e-4, err
+
+
+@pytest.mark.parametrize('name', VARIANTS)
+def test_variant_unet_forward_vs_reference_golden(name):
+    """ada (KTH), ada_u22 (Cityscapes), wo_ref (SMMNIST) denoisers."""
+    cfg = CONFIGS[name]
+    B = GOLDEN_BATCH.get(name, 2)
+    x, t, cond, fea = unet_inputs(cfg, B=B)
+    eps = gpu_eps(handle(name, max_batch=B), x, t, cond, fea)
+    g = load(f'unet_{name}.npz')['eps']
+    err = np.abs(eps.numpy() - g).max()
+    assert err <= 2e-4, err
+
+
+@pytest.mark.parametrize('name', ['ada_small', 'u22_small', 'woref_small'])
+def test_variant_ddpm_chain_vs_oracle(name):
+    """Three DDPM steps with injected noise through the native sampler loop (graph)
+    against the oracle's p_sample_loop restatement over a 3-step schedule."""
+    cfg = CONFIGS[name]
+    x, _, cond, fea = unet_inputs(cfg, B=2, seed=17)
+    h3 = pkg._lib.Handle(cfg, 3, 2, 0)
+    sd = make_sd(cfg)
+    sd.update(pkg.schedule_buffers(3))
+    h3.load_state(sd)
+    h3.finalize()
+    gen = torch.Generator().manual_seed(3)
+    xT = torch.randn(x.shape, generator=gen)
+    noises = torch.stack([torch.randn(x.shape, generator=gen) for _ in range(3)])
+    out = torch.empty(x.shape, device=DEV)
+    h3.sample(0, [2, 1, 0], None, 0., cond.to(DEV), fea.to(DEV), out, x_T=xT.to(DEV),
+              noise=noises.to(DEV).contiguous(), use_graph=True)
+    torch.cuda.synchronize()
+    O = oracle()
+    with torch.no_grad():
+        ref = O.p_sample_loop(O.schedule(3), lambda xx, tt: O.unet_forward(sd, cfg.as_dict(), xx, tt, cond, fea),
+                              xT, list(noises))
+    err = (out.cpu() - ref).abs().max().item()
+    assert err <= 2e-4, err
 
 
 def test_unet_forward_vs_oracle_other_t():
@@ -212,6 +251,23 @@ def test_decoder_multi_frame_matches_per_frame():
     for t in range(2):
         one = gen.decode_frames(src.to(DEV), fl[:, :, t:t + 1].contiguous(), oc[:, :, t:t + 1].contiguous())
         assert (allf[:, :, t] - one[:, :, 0]).abs().max().item() <= 1e-6
+
+
+@pytest.mark.parametrize('cls,name', [('Unet3DAda', 'ada_small'), ('Unet3DAdaU22', 'u22_small'),
+                                      ('Unet3DWoRef', 'woref_small')])
+def test_variant_drop_in_module(cls, name):
+    """The drop-in variant classes take the reference constructor (module defaults
+    for window / dim_head) and reproduce the golden forward once the state is loaded."""
+    cfg = CONFIGS[name]
+    u = getattr(pkg, cls)(dim=cfg.dim, channels=cfg.channels, dim_mults=cfg.dim_mults, cond_num=cfg.tc,
+                          pred_num=cfg.tp, framesize=cfg.latent).to(DEV)
+    assert u.ucfg.window == cfg.window and u.ucfg.dim_head == cfg.dim_head
+    u.load_state_dict(make_sd(cfg))
+    x, t, cond, fea = unet_inputs(cfg)
+    with torch.no_grad():
+        eps = u(x.to(DEV), t.to(DEV), cond.to(DEV), cond_fea=fea.to(DEV))
+    g = load(f'unet_{name}.npz')['eps']
+    assert np.abs(eps.cpu().numpy() - g).max() <= 2e-4
 
 
 def test_drop_in_api_sample_shapes_and_determinism():

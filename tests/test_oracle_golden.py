@@ -8,7 +8,8 @@ import pytest
 import torch
 
 from oracle import extdm_oracle as O
-from tests.golden_inputs import CONFIGS, GEN_CFG, unet_inputs, decoder_inputs, make_sd, make_gen_sd, PKG
+from tests.golden_inputs import (CONFIGS, GEN_CFG, GOLDEN_BATCH, unet_inputs, decoder_inputs, make_sd, make_gen_sd,
+                                 PKG)
 
 GOLD = os.path.join(os.path.dirname(__file__), 'golden')
 
@@ -37,11 +38,12 @@ def test_quantile_cases():
         np.testing.assert_array_equal(out, g[k + '_out'])
 
 
-@pytest.mark.parametrize('name', ['small', 'bair'])
+@pytest.mark.parametrize('name', list(CONFIGS))
 def test_unet_forward(name):
+    """All four denoisers (u12, ada, ada_u22, wo_ref) at reduced and dataset sizes."""
     cfg = CONFIGS[name]
     sd = make_sd(cfg)
-    x, t, cond, fea = unet_inputs(cfg)
+    x, t, cond, fea = unet_inputs(cfg, B=GOLDEN_BATCH.get(name, 2))
     with torch.no_grad():
         eps = O.unet_forward(sd, cfg.as_dict(), x, t, cond, fea)
     g = load(f'unet_{name}.npz')

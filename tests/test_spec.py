@@ -11,7 +11,7 @@ spec = importlib.import_module(PKG + '.spec')
 GOLD = os.path.join(os.path.dirname(__file__), 'golden')
 
 
-@pytest.mark.parametrize('name', ['small', 'bair'])
+@pytest.mark.parametrize('name', list(CONFIGS))
 def test_unet_keys(name):
     ref = json.load(open(os.path.join(GOLD, 'unet_keys.json')))[name]
     mine = [[n, list(s), d] for n, s, d in spec.unet_spec(CONFIGS[name])]
