@@ -220,12 +220,14 @@ def _bn(out, p, c):
             (f'{p}.running_var', (c,)), (f'{p}.num_batches_tracked', (), 'int64')]
 
 
-def generator_spec(g: GeneratorConfig, prefix=''):
-    """Decoder-side Generator entries (first, down_blocks, up_blocks, bottleneck,
-    final) in reference registration order (generator.py:26-62). The
-    pixelwise_flow_predictor (encoder side) is registered first in
-    the reference and is not listed here."""
+def generator_spec(g: GeneratorConfig, prefix='', lfae=None):
+    """Generator entries in reference registration order (generator.py:26-62).
+    With `lfae` (an LfaeConfig) the pixelwise_flow_predictor, registered first,
+    is included; without it only the decoder-side entries (first, down_blocks,
+    up_blocks, bottleneck, final) are listed."""
     out = []
+    if lfae is not None:
+        _pixelwise_flow_predictor(out, f'{prefix}pixelwise_flow_predictor', lfae)
     be, mf = g.block_expansion, g.max_features
     out += [(f'{prefix}first.conv.weight', (be, g.num_channels, 7, 7)), (f'{prefix}first.conv.bias', (be,))]
     _bn(out, f'{prefix}first.norm', be)
@@ -246,4 +248,150 @@ def generator_spec(g: GeneratorConfig, prefix=''):
         _bn(out, f'{p}.norm1', c)
         _bn(out, f'{p}.norm2', c)
     out += [(f'{prefix}final.weight', (g.num_channels, be, 7, 7)), (f'{prefix}final.bias', (g.num_channels,))]
+    return [(e[0], tuple(e[1]), e[2] if len(e) > 2 else 'float32') for e in out]
+
+
+# ---------------------------------------------------------------------------
+# LFAE encoder side: RegionPredictor, BGMotionPredictor,
+# PixelwiseFlowPredictor — model/LFAE/{region_predictor,bg_motion_predictor,
+# pixelwise_flow_predictor,util}.py
+# ---------------------------------------------------------------------------
+
+@dataclass
+class LfaeConfig:
+    """flow_params.model_params of config/DM/*.yaml (defaults: bair.yaml:34-68)."""
+    num_regions: int = 10
+    num_channels: int = 3
+    estimate_affine: bool = True
+    revert_axis_swap: bool = True
+    image: int = 64
+    # bg_predictor_params
+    bg_block_expansion: int = 32
+    bg_max_features: int = 1024
+    bg_num_blocks: int = 5
+    bg_type: str = 'affine'
+    # region_predictor_params
+    rp_temperature: float = 0.1
+    rp_block_expansion: int = 32
+    rp_max_features: int = 1024
+    rp_scale_factor: float = 0.5
+    rp_num_blocks: int = 5
+    rp_pca_based: bool = True
+    rp_pad: int = 0
+    # generator_params
+    gen_block_expansion: int = 64
+    gen_max_features: int = 512
+    gen_num_down_blocks: int = 2
+    gen_num_bottleneck_blocks: int = 6
+    # generator_params.pixelwise_flow_predictor_params
+    pf_block_expansion: int = 64
+    pf_max_features: int = 1024
+    pf_num_blocks: int = 5
+    pf_scale_factor: float = 0.5
+    pf_use_deformed_source: bool = True
+    pf_use_covar_heatmap: bool = True
+    pf_estimate_occlusion_map: bool = True
+    pf_region_var: float = 0.01
+
+    @classmethod
+    def from_config(cls, config, estimate_occlusion_map=None):
+        """From a loaded config/DM/*.yaml dict. `estimate_occlusion_map` overrides the
+        YAML like valid.py:81 does from the CLI flag."""
+        m = config['flow_params']['model_params']
+        bg, rp, gp = m['bg_predictor_params'], m['region_predictor_params'], m['generator_params']
+        pf = gp['pixelwise_flow_predictor_params']
+        c = cls(num_regions=m['num_regions'], num_channels=m['num_channels'],
+                estimate_affine=m['estimate_affine'], revert_axis_swap=m['revert_axis_swap'],
+                image=config['dataset_params']['frame_shape'],
+                bg_block_expansion=bg['block_expansion'], bg_max_features=bg['max_features'],
+                bg_num_blocks=bg['num_blocks'], bg_type=bg.get('bg_type', 'zero'),
+                rp_temperature=rp['temperature'], rp_block_expansion=rp['block_expansion'],
+                rp_max_features=rp['max_features'], rp_scale_factor=rp.get('scale_factor', 1),
+                rp_num_blocks=rp['num_blocks'], rp_pca_based=rp.get('pca_based', False), rp_pad=rp.get('pad', 3),
+                gen_block_expansion=gp['block_expansion'], gen_max_features=gp['max_features'],
+                gen_num_down_blocks=gp['num_down_blocks'], gen_num_bottleneck_blocks=gp['num_bottleneck_blocks'],
+                pf_block_expansion=pf['block_expansion'], pf_max_features=pf['max_features'],
+                pf_num_blocks=pf['num_blocks'], pf_scale_factor=pf.get('scale_factor', 1),
+                pf_use_deformed_source=pf.get('use_deformed_source', True),
+                pf_use_covar_heatmap=pf.get('use_covar_heatmap', False),
+                pf_estimate_occlusion_map=pf.get('estimate_occlusion_map', False),
+                pf_region_var=pf.get('region_var', 0.01))
+        if estimate_occlusion_map is not None:
+            c.pf_estimate_occlusion_map = bool(estimate_occlusion_map)
+        return c
+
+    def generator(self):
+        return GeneratorConfig(num_channels=self.num_channels, block_expansion=self.gen_block_expansion,
+                               max_features=self.gen_max_features, num_down_blocks=self.gen_num_down_blocks,
+                               num_bottleneck_blocks=self.gen_num_bottleneck_blocks, image=self.image)
+
+    @property
+    def pf_in_features(self):
+        return (self.num_regions + 1) * (self.num_channels * int(self.pf_use_deformed_source) + 1)
+
+    @property
+    def bg_outputs(self):
+        return {'zero': 0, 'shift': 2, 'affine': 6, 'perspective': 8}[self.bg_type]
+
+
+def aa_kernel_size(scale):
+    """AntiAliasInterpolation2d kernel size for `scale` (util.py:224-233)."""
+    sigma = (1 / scale - 1) / 2
+    return 2 * round(sigma * 4) + 1
+
+
+def _conv_bn(out, p, ci, co, k):
+    out += [(f'{p}.conv.weight', (co, ci, k, k)), (f'{p}.conv.bias', (co,))]
+    _bn(out, f'{p}.norm', co)
+
+
+def _hg_encoder(out, p, be, cin, nb, mf):
+    """util.Encoder (util.py:152-168)."""
+    for i in range(nb):
+        ci = cin if i == 0 else min(mf, be * 2 ** i)
+        _conv_bn(out, f'{p}.down_blocks.{i}', ci, min(mf, be * 2 ** (i + 1)), 3)
+
+
+def _hourglass(out, p, be, cin, nb, mf):
+    """util.Hourglass (util.py:171-222); out_filters = be + cin."""
+    _hg_encoder(out, f'{p}.encoder', be, cin, nb, mf)
+    for j, i in enumerate(range(nb)[::-1]):
+        ci = (1 if i == nb - 1 else 2) * min(mf, be * 2 ** (i + 1))
+        _conv_bn(out, f'{p}.decoder.up_blocks.{j}', ci, min(mf, be * 2 ** i), 3)
+
+
+def _pixelwise_flow_predictor(out, p, c: LfaeConfig):
+    cin = c.pf_in_features
+    _hourglass(out, f'{p}.hourglass', c.pf_block_expansion, cin, c.pf_num_blocks, c.pf_max_features)
+    of = c.pf_block_expansion + cin
+    out += [(f'{p}.mask.weight', (c.num_regions + 1, of, 7, 7)), (f'{p}.mask.bias', (c.num_regions + 1,))]
+    if c.pf_estimate_occlusion_map:
+        out += [(f'{p}.occlusion.weight', (1, of, 7, 7)), (f'{p}.occlusion.bias', (1,))]
+    if c.pf_scale_factor != 1:
+        k = aa_kernel_size(c.pf_scale_factor)
+        out += [(f'{p}.down.weight', (c.num_channels, 1, k, k))]
+
+
+def region_predictor_spec(c: LfaeConfig, prefix=''):
+    """RegionPredictor (region_predictor.py:28-60) in registration order."""
+    out = []
+    _hourglass(out, f'{prefix}predictor', c.rp_block_expansion, c.num_channels, c.rp_num_blocks, c.rp_max_features)
+    of = c.rp_block_expansion + c.num_channels
+    out += [(f'{prefix}regions.weight', (c.num_regions, of, 7, 7)), (f'{prefix}regions.bias', (c.num_regions,))]
+    if c.estimate_affine and not c.rp_pca_based:
+        out += [(f'{prefix}jacobian.weight', (4, of, 7, 7)), (f'{prefix}jacobian.bias', (4,))]
+    if c.rp_scale_factor != 1:
+        k = aa_kernel_size(c.rp_scale_factor)
+        out += [(f'{prefix}down.weight', (c.num_channels, 1, k, k))]
+    return [(e[0], tuple(e[1]), e[2] if len(e) > 2 else 'float32') for e in out]
+
+
+def bg_predictor_spec(c: LfaeConfig, prefix=''):
+    """BGMotionPredictor (bg_motion_predictor.py:16-44) in registration order."""
+    out = []
+    if c.bg_type != 'zero':
+        _hg_encoder(out, f'{prefix}encoder', c.bg_block_expansion, 2 * c.num_channels, c.bg_num_blocks,
+                    c.bg_max_features)
+        fin = min(c.bg_max_features, c.bg_block_expansion * 2 ** c.bg_num_blocks)
+        out += [(f'{prefix}fc.weight', (c.bg_outputs, fin)), (f'{prefix}fc.bias', (c.bg_outputs,))]
     return [(e[0], tuple(e[1]), e[2] if len(e) > 2 else 'float32') for e in out]

@@ -32,6 +32,22 @@ def rope_freqs(dim, theta=10000):
     return 1. / (theta ** (torch.arange(0, dim, 2)[:(dim // 2)].float() / dim))
 
 
+def antialias_kernel(channels, k):
+    """AntiAliasInterpolation2d.weight (util.py:224-254) for kernel size k; the
+    sigma that yields k is (k - 1) / 8 for the configs' scales 1/2 and 1/4."""
+    sigma = (k - 1) / 8
+    grids = torch.meshgrid([torch.arange(k, dtype=torch.float32)] * 2, indexing='ij')
+    kern = 1
+    for g in grids:
+        mean = (k - 1) / 2
+        kern = kern * torch.exp(-(g - mean) ** 2 / (2 * sigma ** 2))
+    kern = kern / torch.sum(kern)
+    return kern.view(1, 1, k, k).repeat(channels, 1, 1, 1)
+
+
+_BG_IDENTITY = {2: [0, 0], 6: [1, 0, 0, 0, 1, 0], 8: [1, 0, 0, 0, 1, 0, 0, 0]}
+
+
 def synth_state_dict(spec, seed=1234, window=(2, 4, 4)):
     """Return an ordered dict name -> CPU torch tensor for `spec`."""
     rng = np.random.Generator(np.random.PCG64(seed))
@@ -47,8 +63,26 @@ def synth_state_dict(spec, seed=1234, window=(2, 4, 4)):
         if leaf == 'num_batches_tracked':
             sd[name] = torch.tensor(0, dtype=torch.int64)
             continue
+        if name.endswith('down.weight') and len(shape) == 4 and shape[1] == 1:
+            sd[name] = antialias_kernel(shape[0], shape[2])
+            continue
         n = int(np.prod(shape)) if len(shape) else 1
         z = rng.standard_normal(n, dtype=np.float32)
+        if name.endswith('fc.bias') and n in _BG_IDENTITY:
+            # BGMotionPredictor.fc starts at the identity transform (bg_motion_predictor.py:27-41);
+            # keep it near there so the background grid stays in frame
+            v = np.array(_BG_IDENTITY[n], np.float32) + 0.05 * z
+            sd[name] = torch.from_numpy(v.astype(np.float32).reshape(shape))
+            continue
+        if name.endswith('regions.weight'):
+            # RegionPredictor logits are divided by temperature 0.1: keep them O(1) so the
+            # region heatmaps stay smooth (well-conditioned covariances)
+            sd[name] = torch.from_numpy((0.2 * z / math.sqrt(int(np.prod(shape[1:])))).astype(np.float32)
+                                        .reshape(shape))
+            continue
+        if name.endswith('fc.weight') and shape[0] in _BG_IDENTITY:
+            sd[name] = torch.from_numpy((0.05 * z / math.sqrt(shape[1])).astype(np.float32).reshape(shape))
+            continue
         if leaf == 'running_var':
             v = 0.5 + np.abs(z)
         elif leaf == 'running_mean':

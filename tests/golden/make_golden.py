@@ -22,7 +22,7 @@ REF = '/root/reference'
 
 sys.path.insert(0, REPO)
 from tests.golden_inputs import (CONFIGS, GEN_CFG, VARIANTS, GOLDEN_BATCH, unet_inputs, decoder_inputs,  # noqa: E402
-                                 make_sd, make_gen_sd, PKG)
+                                 make_sd, make_gen_sd, PKG, LFAE_CFG, FD_UNET, make_lfae_sd, video_inputs)
 
 spec = importlib.import_module(PKG + '.spec')
 
@@ -59,6 +59,92 @@ def variants():
         np.savez_compressed(os.path.join(HERE, f'unet_{name}.npz'), eps=eps.numpy())
         print(name, 'eps', tuple(eps.shape), float(eps.abs().mean()))
     with open(os.path.join(HERE, 'unet_keys.json'), 'w') as f:
+        json.dump(keys, f)
+
+
+def lfae_config_dict(lc, ucfg, occ):
+    """A config/DM-style dict with the keys FlowDiffusion reads (values from LfaeConfig)."""
+    return {
+        'dataset_params': {'frame_shape': lc.image,
+                           'train_params': {'cond_frames': ucfg.tc, 'pred_frames': ucfg.tp}},
+        'flow_params': {'model_params': {
+            'num_regions': lc.num_regions, 'num_channels': lc.num_channels, 'estimate_affine': lc.estimate_affine,
+            'revert_axis_swap': lc.revert_axis_swap,
+            'bg_predictor_params': {'block_expansion': lc.bg_block_expansion, 'max_features': lc.bg_max_features,
+                                    'num_blocks': lc.bg_num_blocks, 'bg_type': lc.bg_type},
+            'region_predictor_params': {'temperature': lc.rp_temperature, 'block_expansion': lc.rp_block_expansion,
+                                        'max_features': lc.rp_max_features, 'scale_factor': lc.rp_scale_factor,
+                                        'num_blocks': lc.rp_num_blocks, 'pca_based': lc.rp_pca_based,
+                                        'pad': lc.rp_pad, 'fast_svd': False},
+            'generator_params': {'block_expansion': lc.gen_block_expansion, 'max_features': lc.gen_max_features,
+                                 'num_down_blocks': lc.gen_num_down_blocks,
+                                 'num_bottleneck_blocks': lc.gen_num_bottleneck_blocks, 'skips': True,
+                                 'pixelwise_flow_predictor_params': {
+                                     'block_expansion': lc.pf_block_expansion, 'max_features': lc.pf_max_features,
+                                     'num_blocks': lc.pf_num_blocks, 'scale_factor': lc.pf_scale_factor,
+                                     'use_deformed_source': lc.pf_use_deformed_source,
+                                     'use_covar_heatmap': lc.pf_use_covar_heatmap,
+                                     'estimate_occlusion_map': occ}}}},
+        'diffusion_params': {'model_params': {'null_cond_prob': 0.0, 'use_residual_flow': False,
+                                              'only_use_flow': False, 'sampling_timesteps': 10, 'loss_type': 'l2'}},
+    }
+
+
+def lfae():
+    """LFAE encoder modules and FlowDiffusion.sample_one_video."""
+    import dataclasses
+    from model.LFAE.region_predictor import RegionPredictor
+    from model.LFAE.bg_motion_predictor import BGMotionPredictor
+    from model.LFAE.generator import Generator
+    from model.BaseDM_adaptor.VideoFlowDiffusion_multi_w_ref import FlowDiffusion
+    keys = {}
+    out = {}
+    vid = video_inputs()
+    ref = vid[:, :, 1]
+    for occ in (True, False):
+        lc = dataclasses.replace(LFAE_CFG, pf_estimate_occlusion_map=occ)
+        cfgd = lfae_config_dict(lc, FD_UNET, occ)
+        m = cfgd['flow_params']['model_params']
+        sds = make_lfae_sd(lc)
+        gen = Generator(num_regions=m['num_regions'], num_channels=m['num_channels'],
+                        revert_axis_swap=m['revert_axis_swap'], **m['generator_params']).eval()
+        rp = RegionPredictor(num_regions=m['num_regions'], num_channels=m['num_channels'],
+                             estimate_affine=m['estimate_affine'], **m['region_predictor_params']).eval()
+        bg = BGMotionPredictor(num_channels=m['num_channels'], **m['bg_predictor_params']).eval()
+        tag = 'occ' if occ else 'noocc'
+        for name, mod in (('generator', gen), ('region_predictor', rp), ('bg_predictor', bg)):
+            keys[f'{name}_{tag}'] = [[k, list(v.shape)] for k, v in mod.state_dict().items()]
+            mod.load_state_dict(sds[name], strict=True)
+        with torch.no_grad():
+            src_p = rp(ref)
+            drv_p = rp(vid[:, :, 0])
+            bgp = bg(ref, vid[:, :, 0])
+            g = gen(ref, source_region_params=drv_p if False else src_p, driving_region_params=drv_p, bg_params=bgp)
+            bott = gen.forward_bottle(vid[:, :, 0])
+        if occ:
+            for k in ('shift', 'covar', 'affine', 'heatmap'):
+                out[f'rp_src_{k}'] = src_p[k].numpy()
+                out[f'rp_drv_{k}'] = drv_p[k].numpy()
+            out['bg'] = bgp.numpy()
+            out['bottle'] = bott.numpy()
+        for k in ('optical_flow', 'occlusion_map', 'deformed', 'prediction', 'bottle_neck_feat'):
+            if k in g:
+                out[f'gen_{tag}_{k}'] = g[k].numpy()
+        # the whole sample_one_video with the reference FlowDiffusion (DDIM-10)
+        fd = FlowDiffusion(config=cfgd, pretrained_pth='', is_train=False, dim_mults=FD_UNET.dim_mults,
+                           Unet3D_architecture='DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12').eval()
+        fd.generator.load_state_dict(sds['generator'], strict=True)
+        fd.region_predictor.load_state_dict(sds['region_predictor'], strict=True)
+        fd.bg_predictor.load_state_dict(sds['bg_predictor'], strict=True)
+        fd.unet.load_state_dict(make_sd(FD_UNET), strict=True)
+        torch.manual_seed(31)
+        with torch.no_grad():
+            ret = fd.sample_one_video(cond_scale=1.0, real_vid=vid.clone())
+        for k, v in ret.items():
+            out[f'sov_{tag}_{k}'] = v.numpy()
+        print('lfae', tag, {k: tuple(v.shape) for k, v in ret.items()})
+    np.savez_compressed(os.path.join(HERE, 'lfae.npz'), **out)
+    with open(os.path.join(HERE, 'lfae_keys.json'), 'w') as f:
         json.dump(keys, f)
 
 
@@ -187,10 +273,14 @@ def main():
 
 
 if __name__ == '__main__':
-    if '--variants' in sys.argv:
+    if '--variants' in sys.argv or '--lfae' in sys.argv:
         torch.set_num_threads(8)
         import_reference()
-        variants()
+        if '--variants' in sys.argv:
+            variants()
+        if '--lfae' in sys.argv:
+            lfae()
     else:
         main()
         variants()
+        lfae()

@@ -34,6 +34,11 @@ VARIANTS = ['ada_small', 'ada_kth', 'u22_small', 'u22_city', 'woref_small', 'wor
 # the batch each golden forward is run at
 GOLDEN_BATCH = {'ada_kth': 1, 'u22_city': 1, 'woref_smmnist': 1}
 GEN_CFG = _spec.GeneratorConfig()
+# LFAE encoder side: bair.yaml flow_params (estimate_occlusion_map per test)
+LFAE_CFG = _spec.LfaeConfig()
+# FlowDiffusion.sample_one_video golden: the u12 Unet FlowDiffusion builds (dim 64, 512 ch),
+# a short 2 -> 4 round, DDIM-10 over the 1000-step schedule
+FD_UNET = _spec.UnetConfig(tc=2, tp=4)
 
 
 def make_sd(cfg, seed=1234):
@@ -52,6 +57,29 @@ def unet_inputs(cfg, B=2, seed=99):
     fea = torch.from_numpy(rng.standard_normal((B, cfg.fea_ch, cfg.frames, fs, fs), dtype=np.float32))
     t = torch.tensor([999, 1] + [500] * (B - 2), dtype=torch.long)[:B]
     return x, t, cond, fea
+
+
+def make_lfae_sd(lcfg=LFAE_CFG, seed=2468):
+    """State dicts keyed like the AE checkpoint ('generator', 'region_predictor', 'bg_predictor')."""
+    return {'generator': _w.synth_state_dict(_spec.generator_spec(lcfg.generator(), lfae=lcfg), seed=seed),
+            'region_predictor': _w.synth_state_dict(_spec.region_predictor_spec(lcfg), seed=seed + 1),
+            'bg_predictor': _w.synth_state_dict(_spec.bg_predictor_spec(lcfg), seed=seed + 2)}
+
+
+def video_inputs(B=2, T=2, S=64, seed=8):
+    """Smooth synthetic clips in [0, 1): a low-frequency colour field plus a bright
+    square that moves 3 px per frame (so the region / flow predictors see motion)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    low = torch.from_numpy(rng.random((B, 3, 8, 8), dtype=np.float32))
+    base = torch.nn.functional.interpolate(low, size=(S, S), mode='bilinear', align_corners=False) * 0.6
+    vid = base[:, :, None].repeat(1, 1, T, 1, 1)
+    for b in range(B):
+        y0, x0 = int(rng.integers(8, S // 2)), int(rng.integers(8, S // 2))
+        for t in range(T):
+            y, x = y0 + 3 * t, x0 + 2 * t
+            vid[b, :, t, y:y + S // 4, x:x + S // 4] += 0.35
+    noise = torch.from_numpy(rng.random(vid.shape, dtype=np.float32)) * 0.04
+    return (vid + noise).clamp(0, 0.999)
 
 
 def decoder_inputs(B=2, seed=5):
