@@ -5,4 +5,6 @@ Import with importlib (the directory name is not a Python identifier):
 """
 from . import spec, weights, _lib  # noqa: F401
 from .models import (Unet3D, Unet3DAda, Unet3DAdaU22, Unet3DWoRef, UNET3D_BY_MODULE, GaussianDiffusion,  # noqa: F401
-                     Generator, schedule_buffers, ddim_time_pairs)
+                     schedule_buffers, ddim_time_pairs)
+from .lfae import (Generator, RegionPredictor, BGMotionPredictor, FlowDiffusion,  # noqa: F401
+                   autoregressive_sample)

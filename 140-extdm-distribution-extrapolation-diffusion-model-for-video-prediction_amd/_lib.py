@@ -10,7 +10,10 @@ LIB_PATH = os.path.join(HERE, 'libextdm_hip.so')
 # every symbol include/extdm.h declares
 EXPORTS = ['extdm_create', 'extdm_destroy', 'extdm_last_error', 'extdm_load_weight', 'extdm_finalize',
            'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_bench_layer',
-           'extdm_decode']
+           'extdm_decode', 'extdm_set_lfae', 'extdm_region_params', 'extdm_region_hw', 'extdm_bg_params',
+           'extdm_flow_predict', 'extdm_flow_hw', 'extdm_bottleneck']
+
+BG_TYPES = {'zero': 0, 'shift': 1, 'affine': 2, 'perspective': 3}
 
 SAMPLER_DDPM = 0
 SAMPLER_DDIM = 1
@@ -25,6 +28,16 @@ class ExtdmConfig(ctypes.Structure):
                 ('image', ctypes.c_int), ('num_channels', ctypes.c_int), ('gen_block_expansion', ctypes.c_int),
                 ('gen_max_features', ctypes.c_int), ('gen_num_down_blocks', ctypes.c_int),
                 ('gen_num_bottleneck_blocks', ctypes.c_int)]
+
+
+class ExtdmLfaeConfig(ctypes.Structure):
+    _fields_ = [('num_regions', ctypes.c_int), ('num_channels', ctypes.c_int), ('image', ctypes.c_int),
+                ('revert_axis_swap', ctypes.c_int), ('rp_temperature', ctypes.c_float),
+                ('rp_scale_factor', ctypes.c_float), ('rp_pad', ctypes.c_int), ('rp_num_blocks', ctypes.c_int),
+                ('rp_pca_based', ctypes.c_int), ('bg_type', ctypes.c_int), ('bg_num_blocks', ctypes.c_int),
+                ('pf_scale_factor', ctypes.c_float), ('pf_region_var', ctypes.c_float),
+                ('pf_num_blocks', ctypes.c_int), ('pf_use_covar_heatmap', ctypes.c_int),
+                ('pf_use_deformed_source', ctypes.c_int)]
 
 
 _lib = None
@@ -62,6 +75,20 @@ def load():
     L.extdm_bench_layer.restype = i32
     L.extdm_decode.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]
     L.extdm_decode.restype = i32
+    L.extdm_set_lfae.argtypes = [vp, ctypes.POINTER(ExtdmLfaeConfig)]
+    L.extdm_set_lfae.restype = i32
+    L.extdm_region_params.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.extdm_region_params.restype = i32
+    L.extdm_region_hw.argtypes = [vp]
+    L.extdm_region_hw.restype = i32
+    L.extdm_bg_params.argtypes = [vp, i32, vp, vp, vp, vp]
+    L.extdm_bg_params.restype = i32
+    L.extdm_flow_predict.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.extdm_flow_predict.restype = i32
+    L.extdm_flow_hw.argtypes = [vp]
+    L.extdm_flow_hw.restype = i32
+    L.extdm_bottleneck.argtypes = [vp, i32, vp, vp, vp]
+    L.extdm_bottleneck.restype = i32
     _lib = L
     return L
 
@@ -181,6 +208,45 @@ class Handle:
         ms, fl = ctypes.c_float(), ctypes.c_double()
         check(load().extdm_bench_layer(self.h, B, layer, iters, ctypes.byref(ms), ctypes.byref(fl)))
         return float(ms.value), float(fl.value)
+
+    # ---- LFAE encoder (include/extdm.h) ----
+    def set_lfae(self, lc):
+        c = ExtdmLfaeConfig()
+        c.num_regions, c.num_channels, c.image = lc.num_regions, lc.num_channels, lc.image
+        c.revert_axis_swap = int(lc.revert_axis_swap)
+        c.rp_temperature, c.rp_scale_factor = lc.rp_temperature, lc.rp_scale_factor
+        c.rp_pad, c.rp_num_blocks, c.rp_pca_based = lc.rp_pad, lc.rp_num_blocks, int(lc.rp_pca_based)
+        c.bg_type, c.bg_num_blocks = BG_TYPES[lc.bg_type], lc.bg_num_blocks
+        c.pf_scale_factor, c.pf_region_var = lc.pf_scale_factor, lc.pf_region_var
+        c.pf_num_blocks = lc.pf_num_blocks
+        c.pf_use_covar_heatmap, c.pf_use_deformed_source = int(lc.pf_use_covar_heatmap), int(lc.pf_use_deformed_source)
+        check(load().extdm_set_lfae(self.h, ctypes.byref(c)))
+
+    def region_hw(self):
+        return int(load().extdm_region_hw(self.h))
+
+    def flow_hw(self):
+        return int(load().extdm_flow_hw(self.h))
+
+    def region_params(self, img, shift, covar, affine, u=None, sv=None, heat=None):
+        _require_device(img, shift, covar, affine, u, sv, heat)
+        check(load().extdm_region_params(self.h, img.shape[0], _ptr(img), _ptr(shift), _ptr(covar), _ptr(affine),
+                                         _ptr(u), _ptr(sv), _ptr(heat), _stream()))
+
+    def bg_params(self, src, drv, out):
+        _require_device(src, drv, out)
+        check(load().extdm_bg_params(self.h, out.shape[0], _ptr(src), _ptr(drv), _ptr(out), _stream()))
+
+    def flow_predict(self, src, drv, srcp, bg, flow, occ=None):
+        """drv / srcp: dicts with contiguous 'shift', 'covar', 'affine' device tensors."""
+        _require_device(src, bg, flow, occ, *[d[k] for d in (drv, srcp) for k in ('shift', 'covar', 'affine')])
+        check(load().extdm_flow_predict(self.h, src.shape[0], _ptr(src), _ptr(drv['shift']), _ptr(drv['covar']),
+                                        _ptr(drv['affine']), _ptr(srcp['shift']), _ptr(srcp['covar']),
+                                        _ptr(srcp['affine']), _ptr(bg), _ptr(flow), _ptr(occ), _stream()))
+
+    def bottleneck(self, img, out):
+        _require_device(img, out)
+        check(load().extdm_bottleneck(self.h, img.shape[0], _ptr(img), _ptr(out), _stream()))
 
     def decode(self, ref, flow, out, occ=None, warped=None):
         """ref (B,C,S,S), flow (B,2,T,fh,fw), occ (B,1,T,fh,fw) or None -> out (B,C,T,S,S)."""

@@ -150,4 +150,16 @@ void avgpool2(hipStream_t s, float* out, const float* in, int planes, int Ho, in
 void warp_frames(hipStream_t s, float* out, const float* src, const float* flow, int B, int C, int T, int S,
                  int fh, int fw, long out_sb, long out_sc, long out_st);
 
+// LFAE encoder pieces (lfae.hip)
+void aa_down(hipStream_t s, float* out, const float* in, const float* w, int N, int C, int H, int W, int k,
+             int step);
+void region_stats(hipStream_t s, const float* logits, int NR, int h, int w, float temperature, float* heat,
+                  float* shift, float* covar, float* affine, float* u, float* sv);
+void bg_head(hipStream_t s, const float* feat, int N, int Cin, int HW, const float* fw, const float* fb, int nout,
+             int bg_type, float* out);
+void sparse_motion(hipStream_t s, const float* src, const float* dshift, const float* dcov, const float* daff,
+                   const float* sshift, const float* scov, const float* saff, const float* bg, float* motion,
+                   float* pin, int N, int R, int C, int h, int w, int use_cov, int use_def, int revert, float var);
+void flow_combine(hipStream_t s, const float* logits, const float* motion, int N, int K, int h, int w, float* flow);
+
 }  // namespace extdm

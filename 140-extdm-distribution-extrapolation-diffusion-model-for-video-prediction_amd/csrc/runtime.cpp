@@ -786,6 +786,163 @@ struct ExtdmHandle {
     return o;
   }
 
+  // ------------------------------------------------------------ LFAE encoder
+  // RegionPredictor / BGMotionPredictor / PixelwiseFlowPredictor / forward_bottle
+  // (SURVEY §8 a22). Images are [N][C][S][S]; convs are the conv kernels with
+  // BN(eval)+ReLU folded in; concatenations stay two-source conv inputs.
+  ExtdmLfaeConfig lf{};
+  bool has_lf = false;
+  bool has_rp() const { return has("region_predictor.regions.weight"); }
+  bool has_bgp() const { return has("bg_predictor.fc.weight"); }
+  bool has_pf() const { return has("generator.pixelwise_flow_predictor.mask.weight"); }
+
+  void conv_bn_relu2(const std::string& p, const View& out, const View& in0, const View* in1, int pad, bool up2) {
+    auto ab = bn(p + ".norm");
+    const PackedW& w = up2 ? Pup2(p + ".conv.weight") : P(p + ".conv.weight");
+    conv(out, in0, in1, w, 1, pad, D(p + ".conv.bias"), nullptr, ACT_RELU, ab.first, ab.second, 1);
+  }
+
+  // util.Encoder (util.py:152-168): the input and every DownBlock2d output. The
+  // first block may read a two-source input (BGMotionPredictor's cat(source, driving)).
+  std::vector<View> hg_encoder(const std::string& p, const View& x, const View* x1, int nb) {
+    std::vector<View> outs{x};
+    for (int i = 0; i < nb; ++i) {
+      const std::string q = p + ".down_blocks." + std::to_string(i);
+      const int co = (int)H(q + ".conv.weight").shape[0];
+      const View in = outs.back();
+      View c = alloc_cf(in.B, co, 1, in.H, in.W);
+      conv_bn_relu2(q, c, in, i == 0 ? x1 : nullptr, 1, false);
+      View pl = alloc_cf(in.B, co, 1, in.H / 2, in.W / 2);
+      if (!plan) avgpool2(s, pl.p, c.p, in.B * co, in.H / 2, in.W / 2);
+      outs.push_back(pl);
+    }
+    return outs;
+  }
+
+  // util.Hourglass (util.py:171-222); the output cat(last up block, input) is
+  // returned as its two channel sources. (The decoder's NaN -> 0 fix-up of the
+  // encoder outputs is not applied: finite inputs give finite activations.)
+  std::pair<View, View> hourglass(const std::string& p, const View& x, int nb) {
+    std::vector<View> outs = hg_encoder(p + ".encoder", x, nullptr, nb);
+    View a = outs.back();
+    outs.pop_back();
+    View b;
+    bool two = false;
+    for (int j = 0; j < nb; ++j) {
+      const std::string q = p + ".decoder.up_blocks." + std::to_string(j);
+      const int co = (int)H(q + ".conv.weight").shape[0];
+      View u = alloc_cf(a.B, co, 1, a.H * 2, a.W * 2);
+      conv_bn_relu2(q, u, a, two ? &b : nullptr, 1, true);
+      a = u;
+      b = outs.back();
+      outs.pop_back();
+      two = true;
+    }
+    return {a, b};
+  }
+
+  // AntiAliasInterpolation2d (util.py:224-264), or the input itself at scale 1
+  View antialias(const std::string& wname, const View& x, float scale) {
+    if (scale == 1.f) return x;
+    const int step = (int)(1.f / scale);
+    const int k = (int)H(wname).shape[2];
+    View d = alloc_cf(x.B, x.C, 1, x.H / step, x.W / step);
+    if (!plan) aa_down(s, d.p, x.p, D(wname), x.B, x.C, x.H, x.W, k, step);
+    return d;
+  }
+
+  // RegionPredictor.forward, PCA-based (region_predictor.py:62-150)
+  void region_params(int N, const float* img, float* shift, float* covar, float* affine, float* u, float* sv,
+                     float* heat) {
+    REQUIRE(has_lf && has_rp(), "region predictor weights / config not loaded");
+    REQUIRE(lf.rp_pca_based, "only the PCA-based region predictor is supported (config/DM/*.yaml)");
+    Scope top(arena);
+    const std::string p = "region_predictor.";
+    const int C = lf.num_channels, S = lf.image, R = lf.num_regions;
+    View x = antialias(p + "down.weight", cf_view(const_cast<float*>(img), N, C, 1, S, S), lf.rp_scale_factor);
+    auto hg = hourglass(p + "predictor", x, lf.rp_num_blocks);
+    const int hh = x.H + 2 * lf.rp_pad - 6, ww = x.W + 2 * lf.rp_pad - 6;
+    View lg = alloc_cf(N, R, 1, hh, ww);
+    conv(lg, hg.first, &hg.second, P(p + "regions.weight"), 1, lf.rp_pad, D(p + "regions.bias"));
+    if (!plan) region_stats(s, lg.p, N * R, hh, ww, lf.rp_temperature, heat, shift, covar, affine, u, sv);
+  }
+  int region_hw() const {
+    const int step = lf.rp_scale_factor == 1.f ? 1 : (int)(1.f / lf.rp_scale_factor);
+    return lf.image / step + 2 * lf.rp_pad - 6;
+  }
+
+  // BGMotionPredictor.forward (bg_motion_predictor.py:47-64) -> [N][3][3]
+  void bg_params(int N, const float* src, const float* drv, float* out) {
+    REQUIRE(has_lf, "LFAE config not set");
+    Scope top(arena);
+    if (lf.bg_type == 0 || !has_bgp()) {
+      REQUIRE(lf.bg_type == 0, "background predictor weights not loaded");
+      if (!plan) bg_head(s, nullptr, N, 0, 1, nullptr, nullptr, 0, 0, out);
+      return;
+    }
+    const std::string p = "bg_predictor.";
+    const int C = lf.num_channels, S = lf.image;
+    View a = cf_view(const_cast<float*>(src), N, C, 1, S, S), b = cf_view(const_cast<float*>(drv), N, C, 1, S, S);
+    std::vector<View> outs = hg_encoder(p + "encoder", a, &b, lf.bg_num_blocks);
+    const View& f = outs.back();
+    const int nout = (int)H(p + "fc.weight").shape[0];
+    REQUIRE(f.C <= 2048 && nout <= 8, "background head larger than the kernel supports");
+    if (!plan) bg_head(s, f.p, N, f.C, f.H * f.W, D(p + "fc.weight"), D(p + "fc.bias"), nout, lf.bg_type, out);
+  }
+
+  // PixelwiseFlowPredictor.forward (pixelwise_flow_predictor.py:106-153):
+  // flow [N][2][h][w] (x, y), occ [N][1][h][w] or null
+  void flow_predict(int N, const float* src, const float* dsh, const float* dcov, const float* daff,
+                    const float* ssh, const float* scov, const float* saff, const float* bg, float* flow,
+                    float* occ) {
+    REQUIRE(has_lf && has_pf(), "pixelwise flow predictor weights / config not loaded");
+    Scope top(arena);
+    const std::string p = "generator.pixelwise_flow_predictor.";
+    const int C = lf.num_channels, S = lf.image, R = lf.num_regions, K = R + 1;
+    View x = antialias(p + "down.weight", cf_view(const_cast<float*>(src), N, C, 1, S, S), lf.pf_scale_factor);
+    const int h = x.H, w = x.W;
+    const int per = C * (lf.pf_use_deformed_source ? 1 : 0) + 1;
+    float* motion = arena.alloc((size_t)N * K * h * w * 2);
+    View pin = alloc_cf(N, K * per, 1, h, w);
+    if (!plan)
+      sparse_motion(s, x.p, dsh, dcov, daff, ssh, scov, saff, bg, motion, pin.p, N, R, C, h, w,
+                    lf.pf_use_covar_heatmap, lf.pf_use_deformed_source, lf.revert_axis_swap, lf.pf_region_var);
+    auto hg = hourglass(p + "hourglass", pin, lf.pf_num_blocks);
+    View lg = alloc_cf(N, K, 1, h, w);
+    conv(lg, hg.first, &hg.second, P(p + "mask.weight"), 1, 3, D(p + "mask.bias"));
+    if (!plan) flow_combine(s, lg.p, motion, N, K, h, w, flow);
+    if (occ) {
+      REQUIRE(has(p + "occlusion.weight"), "occlusion head not loaded (estimate_occlusion_map=False)");
+      conv(cf_view(occ, N, 1, 1, h, w), hg.first, &hg.second, P(p + "occlusion.weight"), 1, 3,
+           D(p + "occlusion.bias"), nullptr, ACT_SIGMOID);
+    }
+  }
+  int flow_hw() const {
+    const int step = lf.pf_scale_factor == 1.f ? 1 : (int)(1.f / lf.pf_scale_factor);
+    return lf.image / step;
+  }
+
+  // Generator.forward_bottle / compute_fea (generator.py:95-102, 202-206)
+  void bottleneck(int N, const float* img, float* out) {
+    REQUIRE(has_decoder(), "decoder weights (generator.*) not loaded");
+    Scope top(arena);
+    const std::string g = "generator.";
+    const int C = cfg.num_channels, S = cfg.image;
+    const int be = cfg.gen_block_expansion, mf = cfg.gen_max_features, nd = cfg.gen_num_down_blocks;
+    View cur = alloc_cf(N, be, 1, S, S);
+    conv_bn_relu(g + "first", cur, cf_view(const_cast<float*>(img), N, C, 1, S, S), 3);
+    int Sc = S;
+    for (int i = 0; i < nd; ++i) {
+      const int co = std::min(mf, be << (i + 1));
+      View t = alloc_cf(N, co, 1, Sc, Sc);
+      conv_bn_relu(g + "down_blocks." + std::to_string(i), t, cur, 1);
+      View pl = i == nd - 1 ? cf_view(out, N, co, 1, Sc / 2, Sc / 2) : alloc_cf(N, co, 1, Sc / 2, Sc / 2);
+      if (!plan) avgpool2(s, pl.p, t.p, N * co, Sc / 2, Sc / 2);
+      cur = pl;
+      Sc /= 2;
+    }
+  }
+
   // ------------------------------------------------------------ finalize
   void build_tables() {
     const int NT = cfg.timesteps;
@@ -939,8 +1096,20 @@ struct ExtdmHandle {
     if (has_decoder()) {
       arena.top = 0;
       const int fl = cfg.latent > 0 ? cfg.latent : cfg.image / 2;
-      decode(B, cfg.tc + cfg.tp, cfg.image, fl, fl, nullptr, nullptr, reinterpret_cast<const float*>(16), nullptr,
-             nullptr);
+      decode(B, std::max(1, cfg.tc + cfg.tp), cfg.image, fl, fl, nullptr, nullptr,
+             reinterpret_cast<const float*>(16), nullptr, nullptr);
+      arena.top = 0;
+      bottleneck(B, nullptr, nullptr);
+    }
+    if (has_lf) {
+      float* fake = reinterpret_cast<float*>(16);
+      if (has_rp()) { arena.top = 0; region_params(B, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr); }
+      if (has_bgp()) { arena.top = 0; bg_params(B, nullptr, nullptr, nullptr); }
+      if (has_pf()) {
+        arena.top = 0;
+        flow_predict(B, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                     has("generator.pixelwise_flow_predictor.occlusion.weight") ? fake : nullptr);
+      }
     }
     plan = false;
     arena.planning = false;
@@ -1213,6 +1382,67 @@ int extdm_decode(ExtdmHandle* h, int B, int C, int T, int S, int fh, int fw, con
       REQUIRE(C == h->cfg.num_channels && S == h->cfg.image, "decode geometry differs from the config");
     }
     h->decode(B, T, S, fh, fw, ref, flow, occ, pred, warped);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int extdm_set_lfae(ExtdmHandle* h, const ExtdmLfaeConfig* c) {
+  return guarded([&] {
+    REQUIRE(h && c, "null argument");
+    REQUIRE(!h->finalized, "set the LFAE config before extdm_finalize");
+    REQUIRE(c->num_regions >= 1 && c->num_channels >= 1 && c->image >= 8, "bad LFAE config");
+    REQUIRE(c->bg_type >= 0 && c->bg_type <= 3, "bg_type must be 0..3");
+    h->lf = *c;
+    h->has_lf = true;
+  });
+}
+
+#define LFAE_PRELUDE(N)                                                      \
+  REQUIRE(h, "null handle");                                                 \
+  REQUIRE(h->finalized, "handle not finalized");                             \
+  REQUIRE((N) >= 1 && (N) <= h->cfg.max_batch, "batch exceeds max_batch");   \
+  HIPCHK(hipSetDevice(h->cfg.device));                                       \
+  h->s = reinterpret_cast<hipStream_t>(stream)
+
+int extdm_region_params(ExtdmHandle* h, int N, const float* img, float* shift, float* covar, float* affine,
+                        float* u, float* sv, float* heatmap, void* stream) {
+  return guarded([&] {
+    LFAE_PRELUDE(N);
+    REQUIRE(img && shift && covar && affine, "null argument");
+    h->region_params(N, img, shift, covar, affine, u, sv, heatmap);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int extdm_region_hw(const ExtdmHandle* h) { return h && h->has_lf ? h->region_hw() : -1; }
+int extdm_flow_hw(const ExtdmHandle* h) { return h && h->has_lf ? h->flow_hw() : -1; }
+
+int extdm_bg_params(ExtdmHandle* h, int N, const float* src, const float* drv, float* out, void* stream) {
+  return guarded([&] {
+    LFAE_PRELUDE(N);
+    REQUIRE(out && (h->lf.bg_type == 0 || (src && drv)), "null argument");
+    h->bg_params(N, src, drv, out);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int extdm_flow_predict(ExtdmHandle* h, int N, const float* src, const float* drv_shift, const float* drv_covar,
+                       const float* drv_affine, const float* src_shift, const float* src_covar,
+                       const float* src_affine, const float* bg, float* flow, float* occ, void* stream) {
+  return guarded([&] {
+    LFAE_PRELUDE(N);
+    REQUIRE(src && drv_shift && drv_covar && drv_affine && src_shift && src_covar && src_affine && flow,
+            "null argument");
+    h->flow_predict(N, src, drv_shift, drv_covar, drv_affine, src_shift, src_covar, src_affine, bg, flow, occ);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int extdm_bottleneck(ExtdmHandle* h, int N, const float* img, float* out, void* stream) {
+  return guarded([&] {
+    LFAE_PRELUDE(N);
+    REQUIRE(img && out, "null argument");
+    h->bottleneck(N, img, out);
     HIPCHK(hipGetLastError());
   });
 }

@@ -292,59 +292,3 @@ class GaussianDiffusion(nn.Module):
         fn = self.p_sample_loop if not self.is_ddim_sampling else self.ddim_sample
         return fn(x_cond, (batch_size, 3, num_frames, x_cond.shape[3], x_cond.shape[4]), cond_fea=cond_fea,
                   cond=cond, cond_scale=cond_scale, **kw)
-
-
-class Generator(nn.Module):
-    """LFAE Generator, decoder half (generator.py:26-62, 152-206). Holds the
-    reference's decoder parameters (keys without the encoder-side
-    pixelwise_flow_predictor); `forward_with_flow` runs natively."""
-
-    def __init__(self, num_channels=3, block_expansion=64, max_features=512, num_down_blocks=2,
-                 num_bottleneck_blocks=6, skips=True, image_size=64, seed=4321, **unused):
-        super().__init__()
-        if not skips:
-            raise NotImplementedError('the reference configs use skips=True')
-        self.gcfg = GeneratorConfig(num_channels=num_channels, block_expansion=block_expansion,
-                                    max_features=max_features, num_down_blocks=num_down_blocks,
-                                    num_bottleneck_blocks=num_bottleneck_blocks, image=image_size)
-        spec = generator_spec(self.gcfg)
-        _register_tree(self, spec, synth_state_dict(spec, seed=seed))
-        self._handle = None
-
-    def _h(self, device, B, T):
-        """Native decoder handle sized for B clips x T frames (rebuilt when exceeded)."""
-        key = (device.index or 0,)
-        h = self._handle
-        if h is None or h[0] != key or h[1] < B or h[2] < T or h[3] != self._state_version():
-            ucfg = UnetConfig(tc=1, tp=max(T, 2) - 1, latent=self.gcfg.image // 2)
-            nh = _lib.Handle(ucfg, 1000, B, key[0], gcfg=self.gcfg)
-            nh.load_state({'generator.' + k: v for k, v in self.state_dict().items()})
-            nh.finalize()
-            self._handle = h = (key, B, max(T, 2), self._state_version(), nh)
-        return h[4]
-
-    def _state_version(self):
-        return tuple((p.data_ptr(), p._version) for p in self.parameters())
-
-    @torch.no_grad()
-    def forward_with_flow(self, source_image, optical_flow, occlusion_map):
-        """Reference signature (generator.py:152): optical_flow (B, h, w, 2),
-        occlusion_map (B, 1, h, w) or None. Returns 'prediction' and 'deformed'."""
-        flow = optical_flow.permute(0, 3, 1, 2)[:, :, None]
-        occ = occlusion_map[:, :, None] if occlusion_map is not None else None
-        pred, warped = self.decode_frames(source_image, flow, occ, with_warped=True)
-        return {'prediction': pred[:, :, 0], 'deformed': warped[:, :, 0]}
-
-    @torch.no_grad()
-    def decode_frames(self, source_image, flow, occ=None, with_warped=False):
-        """All frames at once: source_image (B,C,S,S), flow (B,2,T,h,w), occ (B,1,T,h,w)
-        or None -> prediction (B,C,T,S,S) [, deformed]."""
-        src = source_image.float().contiguous()
-        fl = flow.float().contiguous()
-        oc = occ.float().contiguous() if occ is not None else None
-        B, C, S, _ = src.shape
-        T = fl.shape[2]
-        pred = torch.empty(B, C, T, S, S, device=src.device, dtype=torch.float32)
-        warped = torch.empty_like(pred) if with_warped else None
-        self._h(src.device, B, T).decode(src, fl, pred, occ=oc, warped=warped)
-        return (pred, warped) if with_warped else pred

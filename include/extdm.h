@@ -22,8 +22,11 @@
  *                                                   Diffusion.py:180-189, 209-258
  *   extdm_sampler_step   one p_sample / DDIM update given eps
  *                                                   Diffusion.py:145-177, 231-255
- *   extdm_decode         Generator.forward_with_flow (occlusion_map=None path)
- *                                                   LFAE/generator.py:152-206
+ *   extdm_decode         Generator.forward_with_flow   LFAE/generator.py:152-206
+ *   extdm_region_params  RegionPredictor.forward       LFAE/region_predictor.py:62-150
+ *   extdm_bg_params      BGMotionPredictor.forward     LFAE/bg_motion_predictor.py:47-64
+ *   extdm_flow_predict   PixelwiseFlowPredictor.forward LFAE/pixelwise_flow_predictor.py:106-153
+ *   extdm_bottleneck     Generator.forward_bottle      LFAE/generator.py:95-102
  */
 #ifndef EXTDM_H
 #define EXTDM_H
@@ -110,6 +113,47 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
  * ('deformed'). Needs the decoder weights (keys 'generator.*') unless occ is NULL. */
 int extdm_decode(ExtdmHandle* h, int B, int C, int T, int S, int fh, int fw, const float* ref, const float* flow,
                  const float* occ, float* pred, float* warped, void* stream);
+
+/* ---- LFAE encoder ------------------------------------------
+ * flow_params.model_params of config/DM/*.yaml. Set before extdm_finalize on a
+ * handle that holds 'region_predictor.*', 'bg_predictor.*' and/or 'generator.*'
+ * (incl. 'generator.pixelwise_flow_predictor.*') weights. Images are [N][C][S][S]
+ * fp32 device tensors, S = image; N <= max_batch. */
+typedef struct ExtdmLfaeConfig {
+  int num_regions, num_channels, image, revert_axis_swap;
+  float rp_temperature, rp_scale_factor;
+  int rp_pad, rp_num_blocks, rp_pca_based;
+  int bg_type; /* 0 zero, 1 shift, 2 affine, 3 perspective */
+  int bg_num_blocks;
+  float pf_scale_factor, pf_region_var;
+  int pf_num_blocks, pf_use_covar_heatmap, pf_use_deformed_source;
+} ExtdmLfaeConfig;
+int extdm_set_lfae(ExtdmHandle* h, const ExtdmLfaeConfig* c);
+
+/* RegionPredictor.forward, PCA-based (LFAE/region_predictor.py:62-150):
+ * shift [N][R][2], covar [N][R][2][2], affine [N][R][2][2] = U sqrt(S) with
+ * torch.svd's (LAPACK sgesdd) sign convention; u [N][R][2][2], sv [N][R][2] (sqrt of
+ * the singular values, the diagonal of 'd') and heatmap [N][R][h][w] optional (NULL).
+ * extdm_region_hw gives the heatmap side h = w. */
+int extdm_region_params(ExtdmHandle* h, int N, const float* img, float* shift, float* covar, float* affine,
+                        float* u, float* sv, float* heatmap, void* stream);
+int extdm_region_hw(const ExtdmHandle* h);
+
+/* BGMotionPredictor.forward (LFAE/bg_motion_predictor.py:47-64): out [N][3][3]. */
+int extdm_bg_params(ExtdmHandle* h, int N, const float* src, const float* drv, float* out, void* stream);
+
+/* PixelwiseFlowPredictor.forward (LFAE/pixelwise_flow_predictor.py:106-153) for
+ * source images src and the region params above (+ bg [N][3][3] or NULL):
+ * flow [N][2][h][w] (x, y; the reference's optical_flow permuted), occ [N][1][h][w]
+ * or NULL (needs the occlusion head). h = w = extdm_flow_hw(). */
+int extdm_flow_predict(ExtdmHandle* h, int N, const float* src, const float* drv_shift, const float* drv_covar,
+                       const float* drv_affine, const float* src_shift, const float* src_covar,
+                       const float* src_affine, const float* bg, float* flow, float* occ, void* stream);
+int extdm_flow_hw(const ExtdmHandle* h);
+
+/* Generator.forward_bottle / compute_fea (LFAE/generator.py:95-102, 202-206):
+ * out [N][C_bottleneck][S / 2^d][S / 2^d]. */
+int extdm_bottleneck(ExtdmHandle* h, int N, const float* img, float* out, void* stream);
 
 #ifdef __cplusplus
 }

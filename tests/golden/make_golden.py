@@ -22,7 +22,8 @@ REF = '/root/reference'
 
 sys.path.insert(0, REPO)
 from tests.golden_inputs import (CONFIGS, GEN_CFG, VARIANTS, GOLDEN_BATCH, unet_inputs, decoder_inputs,  # noqa: E402
-                                 make_sd, make_gen_sd, PKG, LFAE_CFG, FD_UNET, make_lfae_sd, video_inputs)
+                                 make_sd, make_gen_sd, PKG, LFAE_CFG, FD_UNET, make_lfae_sd, video_inputs,
+                                 lfae_config_dict)
 
 spec = importlib.import_module(PKG + '.spec')
 
@@ -60,34 +61,6 @@ def variants():
         print(name, 'eps', tuple(eps.shape), float(eps.abs().mean()))
     with open(os.path.join(HERE, 'unet_keys.json'), 'w') as f:
         json.dump(keys, f)
-
-
-def lfae_config_dict(lc, ucfg, occ):
-    """A config/DM-style dict with the keys FlowDiffusion reads (values from LfaeConfig)."""
-    return {
-        'dataset_params': {'frame_shape': lc.image,
-                           'train_params': {'cond_frames': ucfg.tc, 'pred_frames': ucfg.tp}},
-        'flow_params': {'model_params': {
-            'num_regions': lc.num_regions, 'num_channels': lc.num_channels, 'estimate_affine': lc.estimate_affine,
-            'revert_axis_swap': lc.revert_axis_swap,
-            'bg_predictor_params': {'block_expansion': lc.bg_block_expansion, 'max_features': lc.bg_max_features,
-                                    'num_blocks': lc.bg_num_blocks, 'bg_type': lc.bg_type},
-            'region_predictor_params': {'temperature': lc.rp_temperature, 'block_expansion': lc.rp_block_expansion,
-                                        'max_features': lc.rp_max_features, 'scale_factor': lc.rp_scale_factor,
-                                        'num_blocks': lc.rp_num_blocks, 'pca_based': lc.rp_pca_based,
-                                        'pad': lc.rp_pad, 'fast_svd': False},
-            'generator_params': {'block_expansion': lc.gen_block_expansion, 'max_features': lc.gen_max_features,
-                                 'num_down_blocks': lc.gen_num_down_blocks,
-                                 'num_bottleneck_blocks': lc.gen_num_bottleneck_blocks, 'skips': True,
-                                 'pixelwise_flow_predictor_params': {
-                                     'block_expansion': lc.pf_block_expansion, 'max_features': lc.pf_max_features,
-                                     'num_blocks': lc.pf_num_blocks, 'scale_factor': lc.pf_scale_factor,
-                                     'use_deformed_source': lc.pf_use_deformed_source,
-                                     'use_covar_heatmap': lc.pf_use_covar_heatmap,
-                                     'estimate_occlusion_map': occ}}}},
-        'diffusion_params': {'model_params': {'null_cond_prob': 0.0, 'use_residual_flow': False,
-                                              'only_use_flow': False, 'sampling_timesteps': 10, 'loss_type': 'l2'}},
-    }
 
 
 def lfae():

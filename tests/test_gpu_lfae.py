@@ -1,0 +1,115 @@
+"""GPU parity of the native LFAE encoder and the FlowDiffusion.sample_one_video /
+autoregressive driver mirrors against the reference's own
+outputs (tests/golden/lfae.npz).
+
+Tolerances (fp32): encoder outputs 1e-4 abs (region heatmaps 1e-6: they are
+~1/676); a whole sample_one_video round (encoder, DDIM-10, decode) 1e-3 abs.
+"""
+import dataclasses
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_inputs import (FD_UNET, LFAE_CFG, PKG, lfae_config_dict, make_lfae_sd, make_sd, video_inputs)
+from tests.test_lfae_oracle import gold
+
+pytestmark = pytest.mark.gpu
+
+pkg = importlib.import_module(PKG)
+DEV = torch.device('cuda:0')
+
+
+def fdiff(occ):
+    lc = dataclasses.replace(LFAE_CFG, pf_estimate_occlusion_map=occ)
+    fd = pkg.FlowDiffusion(config=lfae_config_dict(lc, FD_UNET, occ), is_train=False,
+                           dim_mults=FD_UNET.dim_mults,
+                           Unet3D_architecture='DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12').to(DEV)
+    sds = make_lfae_sd(lc)
+    fd.generator.load_state_dict(sds['generator'])
+    fd.region_predictor.load_state_dict(sds['region_predictor'])
+    fd.bg_predictor.load_state_dict(sds['bg_predictor'])
+    fd.unet.load_state_dict(make_sd(FD_UNET))
+    return fd
+
+
+def close(a, g, tol, name):
+    err = np.abs(a.detach().cpu().numpy() - g).max()
+    assert err <= tol, (name, err)
+
+
+def test_region_bg_bottleneck():
+    g = gold()
+    fd = fdiff(True)
+    vid = video_inputs().to(DEV)
+    src = fd.region_predictor(vid[:, :, 1].contiguous())
+    drv = fd.region_predictor(vid[:, :, 0].contiguous())
+    for tag, p in (('src', src), ('drv', drv)):
+        close(p['heatmap'], g[f'rp_{tag}_heatmap'], 1e-6, 'heatmap')
+        close(p['shift'], g[f'rp_{tag}_shift'], 1e-5, 'shift')
+        close(p['covar'], g[f'rp_{tag}_covar'], 1e-5, 'covar')
+        close(p['affine'], g[f'rp_{tag}_affine'], 1e-4, 'affine')
+        # affine = u diag(sqrt(s))
+        assert torch.allclose(p['affine'], p['u'] @ p['d'], atol=1e-6)
+    bg = fd.bg_predictor(vid[:, :, 1].contiguous(), vid[:, :, 0].contiguous())
+    close(bg, g['bg'], 1e-5, 'bg')
+    close(fd.generator.forward_bottle(vid[:, :, 0].contiguous()), g['bottle'], 1e-4, 'bottle')
+
+
+@pytest.mark.parametrize('occ', [True, False])
+def test_generator_forward(occ):
+    g = gold()
+    fd = fdiff(occ)
+    vid = video_inputs().to(DEV)
+    ref = vid[:, :, 1].contiguous()
+    src = fd.region_predictor(ref)
+    drv = fd.region_predictor(vid[:, :, 0].contiguous())
+    bg = fd.bg_predictor(ref, vid[:, :, 0].contiguous())
+    out = fd.generator(ref, source_region_params=src, driving_region_params=drv, bg_params=bg)
+    tag = 'occ' if occ else 'noocc'
+    keys = sorted(k[len(f'gen_{tag}_'):] for k in g.files if k.startswith(f'gen_{tag}_'))
+    assert sorted(out) == keys
+    for k in keys:
+        close(out[k], g[f'gen_{tag}_{k}'], 2e-4, k)
+
+
+@pytest.mark.parametrize('occ', [True, False])
+def test_sample_one_video_vs_reference(occ):
+    """The whole round through the drop-in API, with the reference's DDIM noise
+    (torch.manual_seed(31): x_T then one draw per step) injected."""
+    g = gold()
+    fd = fdiff(occ)
+    vid = video_inputs()
+    torch.manual_seed(31)
+    shape = (vid.shape[0], 3, FD_UNET.tp, FD_UNET.latent, FD_UNET.latent)
+    xT = torch.randn(shape)
+    noise = torch.stack([torch.randn(shape) for _ in range(10)])
+    ret = fd.sample_one_video(cond_scale=1.0, real_vid=vid.to(DEV), x_T=xT.to(DEV),
+                              noise=noise.to(DEV).contiguous())
+    tag = 'occ' if occ else 'noocc'
+    keys = sorted(k[len(f'sov_{tag}_'):] for k in g.files if k.startswith(f'sov_{tag}_'))
+    assert sorted(ret) == keys
+    for k in keys:
+        close(ret[k], g[f'sov_{tag}_{k}'], 1e-3, k)
+
+
+def test_autoregressive_driver_rounds_and_sharding():
+    """valid.py:141-186: rounds chain on the last tc decoded frames; with a seed the
+    result of a clip does not depend on how the batch is sharded."""
+    fd = fdiff(True)
+    vid = video_inputs(B=2, T=2).to(DEV)
+    tc, tp = FD_UNET.tc, FD_UNET.tp
+    total = 2 * tp - 1
+    full = pkg.autoregressive_sample(fd, vid, total, num_sample_video=2, seed=77)
+    assert full.shape == (4, 3, tc + total, 64, 64)
+    assert torch.isfinite(full).all()
+    assert torch.equal(full[:, :, :tc], vid.repeat_interleave(2, dim=0)[:, :, :tc])
+    # shard the (b n) batch in two with the matching global sample base
+    parts = [pkg.autoregressive_sample(fd, vid[i:i + 1], total, num_sample_video=2, seed=77, sample_base=2 * i)
+             for i in range(2)]
+    assert torch.equal(torch.cat(parts), full)
+    # round 0 == one sample_one_video call on the cond frames
+    r0 = fd.sample_one_video(1.0, vid.repeat_interleave(2, dim=0)[:, :, :tc].contiguous(), seed=77, sample_base=0,
+                             round_idx=0)['sample_out_vid']
+    assert torch.equal(r0[:, :, -tp:], full[:, :, tc:tc + tp])
