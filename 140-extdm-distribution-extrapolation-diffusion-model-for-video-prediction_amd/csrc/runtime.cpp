@@ -708,8 +708,9 @@ struct ExtdmHandle {
       // occlusion_map=None: every apply_optical returns the warped skip, so the
       // prediction is exactly deform(source)
       if (!plan) {
-        warp_blend(s, pred, ref, N, C, S, flow, nullptr, T, fh, fw, nullptr);
-        if (warped) warp_blend(s, warped, ref, N, C, S, flow, nullptr, T, fh, fw, nullptr);
+        const long sb = (long)C * T * S * S, sc = (long)T * S * S, st = (long)S * S;  // [B][C][T][S][S]
+        warp_frames(s, pred, ref, flow, B, C, T, S, fh, fw, sb, sc, st);
+        if (warped) warp_frames(s, warped, ref, flow, B, C, T, S, fh, fw, sb, sc, st);
       }
       return;
     }

@@ -115,7 +115,7 @@ int extdm_decode(ExtdmHandle* h, int B, int C, int T, int S, int fh, int fw, con
                  const float* occ, float* pred, float* warped, void* stream);
 
 /* ---- LFAE encoder ------------------------------------------
- * flow_params.model_params of config/DM/*.yaml. Set before extdm_finalize on a
+ * flow_params.model_params of the config/DM YAML files. Set before extdm_finalize on a
  * handle that holds 'region_predictor.*', 'bg_predictor.*' and/or 'generator.*'
  * (incl. 'generator.pixelwise_flow_predictor.*') weights. Images are [N][C][S][S]
  * fp32 device tensors, S = image; N <= max_batch. */

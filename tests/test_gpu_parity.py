@@ -270,6 +270,19 @@ def test_variant_drop_in_module(cls, name):
     assert np.abs(eps.cpu().numpy() - g).max() <= 2e-4
 
 
+def test_decoder_multi_frame_no_occlusion_layout():
+    """Without occlusion the multi-frame decode writes [B, C, T, S, S] like the
+    per-frame forward_with_flow calls stacked on dim 2 (sample_one_video's layout)."""
+    src, flow, _ = decoder_inputs()
+    gen = pkg.Generator()
+    fl = torch.stack([flow.permute(0, 3, 1, 2), flow.flip(1).permute(0, 3, 1, 2), -flow.permute(0, 3, 1, 2)],
+                     dim=2).to(DEV).contiguous()
+    allf = gen.decode_frames(src.to(DEV), fl)
+    for t in range(3):
+        one = gen.forward_with_flow(src.to(DEV), fl[:, :, t].permute(0, 2, 3, 1), None)['prediction']
+        assert torch.equal(allf[:, :, t], one)
+
+
 def test_drop_in_api_sample_shapes_and_determinism():
     cfg = CONFIGS['small']
     u = pkg.Unet3D(dim=cfg.dim, channels=512, dim_mults=cfg.dim_mults, cond_num=cfg.tc, pred_num=cfg.tp,
