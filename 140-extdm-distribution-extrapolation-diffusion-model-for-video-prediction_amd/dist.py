@@ -1,0 +1,55 @@
+"""Clip-shard data parallelism for the sampling path.
+
+Samples are independent (per-sample GroupNorm / LayerNorm / adaptor statistics,
+eval BatchNorm, per-sample quantile, attention within a sample), so the global
+'(b n)' batch is split into contiguous slices, one process per GPU, with no
+collective on the data path; the noise stream is keyed by the global sample
+index (`sample_base` = the slice start), so results do not depend on the rank
+count. The one exchange step is the final all-gather of the generated videos
+(RCCL over xGMI when the backend is "nccl").
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank():
+    """(world, rank, local_rank) from the torch.distributed.run environment."""
+    return (int(os.environ.get('WORLD_SIZE', '1')), int(os.environ.get('RANK', '0')),
+            int(os.environ.get('LOCAL_RANK', '0')))
+
+
+def shard(global_batch, world, rank):
+    """Contiguous slice [start, start + count) of the global batch for `rank`;
+    the first global_batch % world ranks take one extra sample."""
+    base, extra = divmod(global_batch, world)
+    count = base + (1 if rank < extra else 0)
+    start = rank * base + min(rank, extra)
+    return start, count
+
+
+def gather_shards(local, global_batch, world):
+    """All-gather the ranks' slices (dim 0) into the global batch in rank order.
+    Uneven slices are padded to the largest one for the collective."""
+    if world == 1:
+        return local
+    cap = -(-global_batch // world)
+    pad = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]] = local
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    out = []
+    for r in range(world):
+        _, n = shard(global_batch, world, r)
+        out.append(parts[r][:n])
+    return torch.cat(out)
+
+
+def max_over_ranks(value, device=None):
+    """The slowest rank's wall time (bench.py's timing rule)."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -22,7 +22,7 @@ from torch import nn
 
 from . import _lib
 from .models import (UNET3D_BY_MODULE, GaussianDiffusion, _register_tree)
-from .spec import (GeneratorConfig, LfaeConfig, UnetConfig, ARCH_U12, ARCH_WO_REF, bg_predictor_spec,
+from .spec import (GeneratorConfig, LfaeConfig, UnetConfig, ARCH_U12, ARCH_ADA_U22, ARCH_WO_REF, bg_predictor_spec,
                    generator_spec, region_predictor_spec)
 from .weights import synth_state_dict
 
@@ -214,8 +214,10 @@ class FlowDiffusion(nn.Module):
     """FlowDiffusion (VideoFlowDiffusion_multi_w_ref.py:18-118), sampling half.
 
     `wrapper` picks the reference wrapper whose sample_one_video is mirrored:
-    'multi_w_ref' (default; u12/u22/ada, channels 256+256, init_noise_conv path)
-    or 'multi1248' (wo_ref, channels 3+256, dim_mults (1,2,4,8))."""
+    'multi_w_ref' (default; u12/u22/ada, channels 256+256, init_noise_conv path),
+    'multi_w_ref_u22' (ada_u22, channels 3+256; VideoFlowDiffusion_multi_w_ref_u22.py:143-510
+    without its hard-wired cuda:0/cuda:1 model split) or 'multi1248' (wo_ref,
+    channels 3+256, dim_mults (1,2,4,8))."""
 
     def __init__(self, config, pretrained_pth="", is_train=False, ddim_sampling_eta=1., timesteps=1000,
                  dim_mults=(1, 2, 4, 4), learn_null_cond=False, use_deconv=True, padding_mode="zeros",
@@ -252,6 +254,9 @@ class FlowDiffusion(nn.Module):
         tc, tp = ds['train_params']['cond_frames'], ds['train_params']['pred_frames']
         if wrapper == 'multi1248':
             arch, channels = ARCH_WO_REF, 3 + 256
+        elif wrapper == 'multi_w_ref_u22':
+            # hard-imports ada_u22 whatever Unet3D_architecture says (multi_w_ref_u22.py:16, 199-213)
+            arch, channels = ARCH_ADA_U22, 3 + 256
         else:
             arch, channels = Unet3D_architecture, 256 + 256
         unet_cls = UNET3D_BY_MODULE[arch]

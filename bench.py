@@ -2,20 +2,21 @@
 
 Workload (BASELINE.json configs[1]): BAIR 64x64 ch3, 2 -> 28 (tc = 2, tp = 14
 per autoregressive round x 2 rounds), DDPM 1000 steps, u12 Unet3D (dim 64,
-dim_mults 1,2,4,4), random-init weights, synthetic inputs resident in HBM.
+dim_mults 1,2,4,4) behind the multi_w_ref FlowDiffusion wrapper, random-init
+weights, synthetic clips resident in HBM. BAIR eval default: no occlusion map
+(valid_DM_bair.sh omits --estimate_occlusion_map).
 
-One bench "step" = one full 2 -> 28 sample of the per-GPU clip batch:
-  for each of the 2 rounds: the DDPM-1000 reverse loop (one captured hipGraph
-  step replayed 1000x: Unet3D forward + fused threshold/posterior/noise step)
-  and the LFAE flow-warp decode of the round's tc + tp frames;
-then (N > 1) an RCCL all-gather of the predicted frames to every rank.
-The LFAE encoder is not in this build yet: round 1 uses
-synthetic flow / bottleneck conditioning and round 2 conditions on round 1's
-last predicted flows (+ zero occlusion channel, the BAIR eval default).
+One bench "step" = the eval driver's full 2 -> 28 generation of the per-GPU clip
+batch (scripts/DM/valid.py:141-186 through the package's autoregressive_sample):
+per round the LFAE encoder on the tc cond frames (region / background / flow
+predictors, bottleneck features), the DDPM-1000 reverse loop (one captured
+hipGraph step replayed 1000x: Unet3D forward + fused threshold/posterior/noise
+step) and the flow-warp decode of the round's tc + tp frames; then (N > 1) an
+RCCL all-gather of the generated videos to every rank.
 
-Clip batches are sharded over ranks (weak scaling, one process per GPU);
-noise is a counter-based Philox stream keyed by the global sample index, so a
-clip's result does not depend on the shard it lands on.
+Clip batches are sharded over ranks (weak scaling, one process per GPU); the
+noise is a counter-based Philox stream keyed by (seed, global sample index,
+round, step), so a clip's result does not depend on the shard it lands on.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 """
@@ -25,6 +26,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -39,46 +41,57 @@ def parse():
     ap.add_argument('--steps', type=int, default=1)
     ap.add_argument('--warmup', type=int, default=0)
     ap.add_argument('--batch', type=int, default=32, help='clips per GPU')
-    ap.add_argument('--sampling-steps', type=int, default=1000)
-    ap.add_argument('--rounds', type=int, default=2)
+    ap.add_argument('--sampling-steps', type=int, default=1000,
+                    help='1000 = DDPM-1000 (the metric); fewer = DDIM-S (profiling sweeps only)')
+    ap.add_argument('--total-pred', type=int, default=28)
+    ap.add_argument('--tp', type=int, default=14)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=4)
     return ap.parse_args()
 
 
-def cpu_baseline(ucfg, rounds, steps_per_round, n_steps):
+def synthetic_clips(B, tc, S, seed):
+    """Conditioning clips U[0,1) from NumPy PCG64."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return torch.from_numpy(rng.random((B, 3, tc, S, S), dtype=np.float32))
+
+
+def cpu_baseline(pkg, fd, rounds, steps_per_round, n_steps):
     """The oracle (PyTorch-CPU restatement of the reference) timed on this box's
-    host cores: B = 1, n_steps DDPM steps (Unet forward + p_sample update) and
-    one round's decode, extrapolated to frames/s for the same 2 -> 28 workload."""
+    host cores at B = 1: one round's LFAE encoder, n_steps DDPM steps (Unet
+    forward + p_sample update) and one round's decode, extrapolated to the same
+    2 -> 28 workload."""
+    import dataclasses
     from oracle import extdm_oracle as O
-    import importlib
-    pkg = importlib.import_module(PKG)
-    torch.manual_seed(0)
-    sd = pkg.weights.synth_state_dict(pkg.spec.unet_spec(ucfg), seed=1234)
+    from oracle import lfae_oracle as LO
+    ucfg = fd.unet.ucfg
+    lc = dataclasses.replace(fd.lcfg)
+    sd = {f'generator.{k}': v.detach().cpu() for k, v in fd.generator.state_dict().items()}
+    sd.update({f'region_predictor.{k}': v.detach().cpu() for k, v in fd.region_predictor.state_dict().items()})
+    sd.update({f'bg_predictor.{k}': v.detach().cpu() for k, v in fd.bg_predictor.state_dict().items()})
+    usd = {k: v.detach().cpu() for k, v in fd.unet.state_dict().items()}
     sch = O.schedule(1000)
-    L, fs = ucfg.latent, ucfg.fea_size
-    x = torch.randn(1, 3, ucfg.tp, L, L)
-    cond = torch.rand(1, 3, ucfg.tc, L, L) * 2 - 1
-    fea = torch.randn(1, 256, ucfg.tc + ucfg.tp, fs, fs)
+    vid = synthetic_clips(1, ucfg.tc, lc.image, 99)
     with torch.no_grad():
+        t0 = time.perf_counter()
+        ret, x_cond, fea, ref = LO.encode_round(sd, lc, ucfg, vid)
+        t_enc = time.perf_counter() - t0
+        x = torch.randn(1, 3, ucfg.tp, ucfg.latent, ucfg.latent)
         t = torch.full((1,), 999, dtype=torch.long)
-        O.ddpm_step(sch, x, O.unet_forward(sd, ucfg.as_dict(), x, t, cond, fea), t, torch.randn_like(x))  # warm
+        O.ddpm_step(sch, x, O.unet_forward(usd, ucfg.as_dict(), x, t, x_cond, fea), t, torch.randn_like(x))  # warm
         t0 = time.perf_counter()
         for k in range(n_steps):
             t = torch.full((1,), 998 - k, dtype=torch.long)
-            x = O.ddpm_step(sch, x, O.unet_forward(sd, ucfg.as_dict(), x, t, cond, fea), t, torch.randn_like(x))
+            x = O.ddpm_step(sch, x, O.unet_forward(usd, ucfg.as_dict(), x, t, x_cond, fea), t, torch.randn_like(x))
         t_step = (time.perf_counter() - t0) / n_steps
-        src = torch.rand(1, 3, 64, 64)
-        flow = torch.rand(1, 32, 32, 2) * 2 - 1
         t0 = time.perf_counter()
-        for _ in range(ucfg.tc + ucfg.tp):
-            O.deform(src, flow)
+        LO.decode_round(sd, lc, ucfg, ret, x, ref)
         t_dec = time.perf_counter() - t0
-    total = rounds * (steps_per_round * t_step + t_dec)
+    total = rounds * (t_enc + steps_per_round * t_step + t_dec)
     return {'value': rounds * ucfg.tp / total, 'unit': 'frames/s', 'cores': torch.get_num_threads(),
             'kind': 'port',
-            'sample': f'oracle B=1: {n_steps} DDPM steps ({t_step:.3f} s/step) + one round decode '
-                      f'({t_dec:.4f} s), extrapolated to {rounds} rounds x {steps_per_round} steps'}
+            'sample': f'oracle B=1: encoder round ({t_enc:.3f} s), {n_steps} DDPM steps ({t_step:.3f} s/step), '
+                      f'decode round ({t_dec:.3f} s); extrapolated to {rounds} rounds x {steps_per_round} steps'}
 
 
 def main():
@@ -93,45 +106,31 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
     import importlib
     pkg = importlib.import_module(PKG)
-    ucfg = pkg.spec.UnetConfig()  # BAIR u12
-    B = args.batch
-    S = args.sampling_steps
-    tc, tp, L, fs = ucfg.tc, ucfg.tp, ucfg.latent, ucfg.fea_size
+    B, S_steps = args.batch, args.sampling_steps
+    wrapper, unet_arch = pkg.configs.dm_arch('bair')
+    cfg = pkg.configs.dm_config('bair', pred_frames=args.tp, sampling_timesteps=S_steps,
+                                estimate_occlusion_map=False)
+    fd = pkg.FlowDiffusion(config=cfg, is_train=False, Unet3D_architecture=unet_arch, wrapper=wrapper).to(dev)
+    fd.diffusion.max_batch = B
+    tc, tp = fd.cond_frame_num, fd.pred_frame_num
+    rounds = -(-args.total_pred // tp)
+    clips = synthetic_clips(B, tc, 64, 1234 + rank).to(dev)
 
-    h = pkg._lib.Handle(ucfg, 1000, B, local)
-    sd = pkg.weights.synth_state_dict(pkg.spec.unet_spec(ucfg), seed=1234)
-    sd.update(pkg.schedule_buffers(1000))
-    h.load_state(sd)
-    h.finalize()
-    gen = pkg.Generator()
-
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    x_cond0 = torch.cat([torch.rand(B, 2, tc, L, L, device=dev, generator=g) * 2 - 1,
-                         torch.zeros(B, 1, tc, L, L, device=dev)], dim=1).contiguous()
-    fea = torch.randn(B, 256, tc + tp, fs, fs, device=dev, generator=g).contiguous()
-    ref_img = torch.rand(B, 3, 64, 64, device=dev, generator=g).contiguous()
-    out_vid = torch.empty(B, 3, args.rounds * tp, 64, 64, device=dev)
-    times = list(range(S - 1, -1, -1)) if S == 1000 else [int(round(999 * (1 - k / max(S - 1, 1)))) for k in range(S)]
+    D = pkg.dist
+    start, count = D.shard(world * B, world, rank)  # weak scaling: B clips per rank
 
     def one_step(step_idx):
-        x_cond = x_cond0
-        for r in range(args.rounds):
-            pred = torch.empty(B, 3, tp, L, L, device=dev)
-            h.sample(pkg._lib.SAMPLER_DDPM, times, None, 0., x_cond, fea, pred, seed=1234 + step_idx,
-                     sample_base=rank * B, round_idx=r)
-            flows = torch.cat([x_cond[:, :2], pred[:, :2]], dim=2).contiguous()
-            frames = gen.decode_frames(ref_img, flows)  # (B, 3, tc + tp, 64, 64)
-            out_vid[:, :, r * tp:(r + 1) * tp] = frames[:, :, tc:]
-            x_cond = torch.cat([pred[:, :2, -tc:], torch.zeros(B, 1, tc, L, L, device=dev)], dim=1).contiguous()
-        if world > 1:
-            allv = torch.empty((world,) + tuple(out_vid.shape), device=dev)
-            torch.distributed.all_gather_into_tensor(allv, out_vid)
-        return out_vid
+        out = pkg.autoregressive_sample(fd, clips, args.total_pred, num_sample_video=1, seed=1234 + step_idx,
+                                        sample_base=start)
+        return D.gather_shards(out.contiguous(), world * B, world)  # RCCL all-gather over xGMI
 
-    # prime: load every kernel and capture / replay the step graph once (2 denoising steps, untimed)
-    prime = torch.empty(B, 3, tp, L, L, device=dev)
-    h.sample(pkg._lib.SAMPLER_DDPM, times[:2], None, 0., x_cond0, fea, prime, seed=1, sample_base=rank * B)
-    gen.decode_frames(ref_img, torch.cat([x_cond0[:, :2], prime[:, :2]], dim=2).contiguous())
+    # prime (untimed): build every native handle, load kernels, capture + replay the
+    # step graph once on a 2-step schedule, run the encoder and the decoder
+    ret, x_cond, fea, ref = fd.encode(clips)
+    h = fd.diffusion._native(B, dev)
+    prime = torch.empty(B, 3, tp, x_cond.shape[3], x_cond.shape[4], device=dev)
+    h.sample(pkg._lib.SAMPLER_DDPM, [999, 998], None, 0., x_cond, fea, prime, seed=1, sample_base=start)
+    fd.decode(ret, prime, ref)
     for w in range(args.warmup):
         one_step(-1 - w)
     if world > 1:
@@ -139,21 +138,17 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        one_step(k)
+        out = one_step(k)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([el], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        el = float(tt.item())
-    frames = world * B * args.rounds * tp * args.steps
+    el = D.max_over_ranks(time.perf_counter() - t0, device=dev)
+    frames = world * B * args.total_pred * args.steps
     value = frames / el
 
     result = None
     if rank == 0:
-        assert torch.isfinite(out_vid).all()
+        assert torch.isfinite(out).all()
         ms_layer, flops = h.bench_layer(B, 0, 20)
         achieved = flops / (ms_layer * 1e-3) / 1e12
         traffic = None
@@ -163,25 +158,27 @@ def main():
                 j = json.load(open(pmc))
                 if int(j.get('batch', -1)) == B:
                     traffic = j.get('hbm_bytes_per_launch')
-            except Exception:
+            except (ValueError, OSError):
                 traffic = None
         meta = json.load(open(os.path.join(REPO, 'BASELINE.json')))
+        sampler = 'DDPM 1000' if S_steps >= 1000 else f'DDIM {S_steps}'
         result = {
             'metric': meta['metric'], 'value': round(value, 4), 'unit': 'frames/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 2),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
-            'data': 'synthetic (seeded random-init weights, synthetic conditioning; no dataset/checkpoint offline)',
-            'config': {'workload': f'BAIR 64x64 ch3 2->{args.rounds * tp} (tc={tc}, tp={tp} x {args.rounds} rounds), '
-                                   f'DDPM {S} steps, u12 Unet3D dim 64 mults (1,2,4,4)',
-                       'global_batch': world * B, 'batch_per_gpu': B, 'sampling_steps': S,
-                       'rounds': args.rounds, 'parallelism': f'clip-shard x{world} (+RCCL all-gather)',
+            'data': 'synthetic (U[0,1) PCG64 clips, seeded random-init weights; no dataset/checkpoint offline)',
+            'config': {'workload': f'BAIR 64x64 ch3 {tc}->{args.total_pred} (tp={tp} x {rounds} rounds), '
+                                   f'{sampler} steps, u12 Unet3D dim 64 mults (1,2,4,4), LFAE encoder + '
+                                   f'flow-warp decoder, no occlusion map (BAIR eval default)',
+                       'global_batch': world * B, 'batch_per_gpu': B, 'sampling_steps': S_steps,
+                       'rounds': rounds, 'parallelism': f'clip-shard x{world} (+RCCL all-gather)',
                        'workspace_gb': round(h.workspace_bytes() / 2 ** 30, 2)},
             'roofline': {'bound': 'mfma', 'kernel': 'conv_halo_kernel<7,64,1> (init_conv 512->64, 1x7x7)',
                          'achieved': round(achieved, 2), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic},
         }
         if not args.no_cpu_baseline and world == 1:
-            result['cpu_baseline'] = cpu_baseline(ucfg, args.rounds, 1000, args.cpu_steps)
+            result['cpu_baseline'] = cpu_baseline(pkg, fd, rounds, 1000, args.cpu_steps)
         print(json.dumps(result))
     if world > 1:
         torch.distributed.destroy_process_group()
