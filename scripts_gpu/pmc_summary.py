@@ -1,0 +1,28 @@
+"""Per-launch HBM bytes of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE,
+WRITE_SIZE; KB units), with the gfx950 correction of MI355X_MICROARCH.md (HBM
+section): FETCH_SIZE counts half the bytes of 16-B/lane streaming reads -> x2."""
+import csv
+import glob
+import json
+import sys
+
+fetch_dir, write_dir, pattern, batch, out = sys.argv[1:6]
+
+
+def rows(d, counter):
+    vals = []
+    for f in glob.glob(f'{d}/**/*counter_collection.csv', recursive=True):
+        for r in csv.DictReader(open(f)):
+            if pattern in r.get('Kernel_Name', '') and r.get('Counter_Name') == counter:
+                vals.append(float(r['Counter_Value']))
+    return vals
+
+
+fe = rows(fetch_dir, 'FETCH_SIZE')
+wr = rows(write_dir, 'WRITE_SIZE')
+res = {'kernel': pattern, 'batch': int(batch), 'launches': [len(fe), len(wr)],
+       'fetch_kb_raw_per_launch': sum(fe) / max(len(fe), 1), 'write_kb_per_launch': sum(wr) / max(len(wr), 1)}
+res['hbm_bytes_per_launch'] = int(2 * res['fetch_kb_raw_per_launch'] * 1024 + res['write_kb_per_launch'] * 1024)
+res['note'] = 'FETCH_SIZE doubled (gfx950 streaming-read correction); KB = 1024 B'
+json.dump(res, open(out, 'w'), indent=1)
+print(json.dumps(res))
