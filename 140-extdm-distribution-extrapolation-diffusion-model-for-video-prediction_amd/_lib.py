@@ -11,12 +11,16 @@ LIB_PATH = os.path.join(HERE, 'libextdm_hip.so')
 EXPORTS = ['extdm_create', 'extdm_destroy', 'extdm_last_error', 'extdm_load_weight', 'extdm_finalize',
            'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_bench_layer',
            'extdm_decode', 'extdm_set_lfae', 'extdm_region_params', 'extdm_region_hw', 'extdm_bg_params',
-           'extdm_flow_predict', 'extdm_flow_hw', 'extdm_bottleneck']
+           'extdm_flow_predict', 'extdm_flow_hw', 'extdm_bottleneck', 'extdm_range_flag']
 
 BG_TYPES = {'zero': 0, 'shift': 1, 'affine': 2, 'perspective': 3}
 
 SAMPLER_DDPM = 0
 SAMPLER_DDIM = 1
+
+# include/extdm.h EXTDM_PRECISION_*: arithmetic of the direct convolutions
+PRECISIONS = {'fp32': 0, 'f16x3': 1}
+DEFAULT_PRECISION = os.environ.get('EXTDM_PRECISION', 'f16x3')
 
 
 class ExtdmConfig(ctypes.Structure):
@@ -27,7 +31,7 @@ class ExtdmConfig(ctypes.Structure):
                 ('timesteps', ctypes.c_int), ('max_batch', ctypes.c_int), ('device', ctypes.c_int),
                 ('image', ctypes.c_int), ('num_channels', ctypes.c_int), ('gen_block_expansion', ctypes.c_int),
                 ('gen_max_features', ctypes.c_int), ('gen_num_down_blocks', ctypes.c_int),
-                ('gen_num_bottleneck_blocks', ctypes.c_int)]
+                ('gen_num_bottleneck_blocks', ctypes.c_int), ('precision', ctypes.c_int)]
 
 
 class ExtdmLfaeConfig(ctypes.Structure):
@@ -89,6 +93,8 @@ def load():
     L.extdm_flow_hw.restype = i32
     L.extdm_bottleneck.argtypes = [vp, i32, vp, vp, vp]
     L.extdm_bottleneck.restype = i32
+    L.extdm_range_flag.argtypes = [vp, i32, vp]
+    L.extdm_range_flag.restype = i32
     _lib = L
     return L
 
@@ -120,7 +126,7 @@ def _require_device(*tensors):
 class Handle:
     """One native model instance (Unet3D weights + diffusion buffers [+ decoder])."""
 
-    def __init__(self, ucfg, timesteps, max_batch, device=0, gcfg=None):
+    def __init__(self, ucfg, timesteps, max_batch, device=0, gcfg=None, precision=None):
         L = load()
         c = ExtdmConfig()
         from .spec import ARCH_IDS
@@ -151,6 +157,10 @@ class Handle:
         c.gen_max_features = gcfg.max_features
         c.gen_num_down_blocks = gcfg.num_down_blocks
         c.gen_num_bottleneck_blocks = gcfg.num_bottleneck_blocks
+        self.precision = precision or DEFAULT_PRECISION
+        if self.precision not in PRECISIONS:
+            raise ValueError(f'precision must be one of {sorted(PRECISIONS)}, got {self.precision!r}')
+        c.precision = PRECISIONS[self.precision]
         self.cfg = ucfg
         self.max_batch = max_batch
         self.timesteps = timesteps
@@ -203,6 +213,13 @@ class Handle:
         _require_device(x, eps, noise, thresh_out)
         check(load().extdm_sampler_step(self.h, x.shape[0], sampler, int(t), int(t_next), float(eta), _ptr(x),
                                         _ptr(eps), _ptr(noise), _ptr(thresh_out), _stream()))
+
+    def range_flag(self, reset=True):
+        """1 if an f16x3 conv input reached |v| >= 65504 since the last reset."""
+        rc = load().extdm_range_flag(self.h, 1 if reset else 0, _stream())
+        if rc < 0:
+            check(rc)
+        return rc
 
     def bench_layer(self, B, layer=0, iters=20):
         ms, fl = ctypes.c_float(), ctypes.c_double()

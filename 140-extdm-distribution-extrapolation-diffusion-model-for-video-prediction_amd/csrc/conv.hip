@@ -235,6 +235,8 @@ void launch_bm(hipStream_t s, const ConvArgs& a, int bm, dim3 grid_n) {
 
 void conv_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                   int stride, int pad, const ConvEpi& epi) {
+  if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 && conv_x3_forward(s, out, in0, in1, w, epi))
+    return;
   if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 && !getenv_flag("EXTDM_NO_HALO") &&
       conv_halo_forward(s, out, in0, in1, w, epi))
     return;

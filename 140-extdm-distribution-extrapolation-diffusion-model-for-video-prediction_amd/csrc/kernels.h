@@ -45,6 +45,11 @@ struct PackedW {
   // direct-conv (halo tile) layout [mtile][stage][step][half][BM], see conv_halo.hip
   float* wh = nullptr;
   int hstages = 0, hbm = 0;
+  // f16x3 split layout [mtile][cblock*KS + ky][(g, kx)][m32][hi|lo][lane][8] (conv_x3.hip),
+  // rows pre-scaled by powers of two undone by xscale[m]
+  void* wx = nullptr;
+  float* xscale = nullptr;
+  int xbm = 0, xbn = 0, xng = 0, xncgb = 0;
 };
 
 // Output-channel tile of the conv GEMM for M output channels (Mpad is a multiple of it).
@@ -65,6 +70,15 @@ int halo_ch(int ks, int bm);
 // Direct stride-1 'same' conv through LDS halo tiles; false if the geometry is not covered.
 bool conv_halo_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                        const ConvEpi& epi);
+
+// f16x3 split-precision direct conv (conv_x3.hip): tile choice, launch (false if
+// the geometry is not covered), and the activation-range flag (|v| >= 65504 seen).
+struct X3Tile { int bm, bn, ng; };
+X3Tile x3_tile(int ks, int cout);
+bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
+                     const ConvEpi& epi);
+void x3_range_reset(hipStream_t s);
+int x3_range_read(hipStream_t s);
 
 // out = act(conv(in0 ++ in1) + bias + res) [* s + sh]
 void conv_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,

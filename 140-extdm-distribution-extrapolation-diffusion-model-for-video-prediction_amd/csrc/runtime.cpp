@@ -156,7 +156,53 @@ struct ExtdmHandle {
     pw.w = dmalloc(a.size() * sizeof(float));
     HIPCHK(hipMemcpy(pw.w, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
     if (kh == kw && (kh == 1 || kh == 3 || kh == 7) && co > 32) pack_halo(pw, t.f, ci);
+    if (cfg.precision == EXTDM_PRECISION_F16X3 && kh == kw && (kh == 1 || kh == 3 || kh == 7) && co > 32 &&
+        ci >= 16)
+      pack_x3(pw, t.f, ci);
     return packed[n] = pw;
+  }
+  // f16x3 layout (conv_x3.hip): [mtile][cb*KS + ky][(g, kx)][m32][hi|lo][lane][8], lane =
+  // (h, lc): row m = mtile*BM + m32*32 + lc, input channel cb*16NG + g*16 + 8h + e. Row m is
+  // scaled by 2^s(m) (max |w| -> [2^14, 2^15)), undone by xscale[m] = 2^-s(m) in the epilogue.
+  void pack_x3(PackedW& pw, const std::vector<float>& w, int ci) {
+    const int ks = pw.KH, kk = ks * ks, co = pw.M;
+    const X3Tile tl = x3_tile(ks, co);
+    const int cib = 16 * tl.ng, ncgb = (ci + cib - 1) / cib, mt = (co + tl.bm - 1) / tl.bm;
+    const int m32 = tl.bm / 32, steps = tl.ng * ks;
+    const size_t ah = (size_t)steps * m32 * 2 * 512;
+    std::vector<float> scale(co), rs(co);
+    for (int m = 0; m < co; ++m) {
+      float mx = 0.f;
+      for (size_t k = 0; k < (size_t)ci * kk; ++k) mx = std::max(mx, std::fabs(w[(size_t)m * ci * kk + k]));
+      int e = 0;
+      if (mx > 0.f) { std::frexp(mx, &e); e = 15 - e; }  // mx * 2^e in [2^14, 2^15)
+      scale[m] = std::ldexp(1.f, e);
+      rs[m] = std::ldexp(1.f, -e);
+    }
+    std::vector<_Float16> a((size_t)mt * ncgb * ks * ah, (_Float16)0.f);
+    for (int mtile = 0; mtile < mt; ++mtile)
+      for (int cb = 0; cb < ncgb; ++cb)
+        for (int ky = 0; ky < ks; ++ky)
+          for (int g = 0; g < tl.ng; ++g)
+            for (int kx = 0; kx < ks; ++kx)
+              for (int q = 0; q < m32; ++q)
+                for (int l = 0; l < 64; ++l)
+                  for (int e = 0; e < 8; ++e) {
+                    const int m = mtile * tl.bm + q * 32 + (l & 31);
+                    const int c = cb * cib + g * 16 + 8 * (l >> 5) + e;
+                    if (m >= co || c >= ci) continue;
+                    const float v = w[((size_t)m * ci + c) * kk + ky * ks + kx] * scale[m];
+                    const _Float16 hi = (_Float16)v;
+                    const _Float16 lo = (_Float16)(v - (float)hi);
+                    const size_t base = (((((size_t)mtile * ncgb + cb) * ks + ky) * steps + g * ks + kx) * m32 + q) * 2;
+                    a[(base + 0) * 512 + l * 8 + e] = hi;
+                    a[(base + 1) * 512 + l * 8 + e] = lo;
+                  }
+    pw.wx = dmalloc(a.size() * sizeof(_Float16));
+    HIPCHK(hipMemcpy(pw.wx, a.data(), a.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    pw.xscale = dmalloc(co * sizeof(float));
+    HIPCHK(hipMemcpy(pw.xscale, rs.data(), co * sizeof(float), hipMemcpyHostToDevice));
+    pw.xbm = tl.bm; pw.xbn = tl.bn; pw.xng = tl.ng; pw.xncgb = ncgb;
   }
   // Direct-conv layout [mtile][stage][step][half][BM]: step = (cp*k + ky)*k + kx,
   // input channel = stage*2CH + half*CH + cp (conv_halo.hip).
@@ -1304,6 +1350,7 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     if (x_T) HIPCHK(hipMemcpyAsync(out, x_T, (size_t)B * n * sizeof(float), hipMemcpyDeviceToDevice, s));
     else fill_normal(s, out, B, n, seed, sample_base, round, 0x7FFFFFFF);
     HIPCHK(hipMemsetAsync(h->step_ctr, 0, sizeof(int), s));
+    if (h->cfg.precision == EXTDM_PRECISION_F16X3) x3_range_reset(s);
     int klo, khi;
     float w;
     h->quantile_ranks(n, klo, khi, w);
@@ -1332,7 +1379,23 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(h->ev_out, s));
     HIPCHK(hipStreamWaitEvent(caller, h->ev_out, 0));
+    REQUIRE(h->cfg.precision != EXTDM_PRECISION_F16X3 || x3_range_read(s) == 0,
+            "f16x3 precision: a conv input reached |v| >= 65504 during sampling; results are not fp32-accurate "
+            "(create the handle with EXTDM_PRECISION_FP32)");
   });
+}
+
+int extdm_range_flag(ExtdmHandle* h, int reset, void* stream) {
+  int flag = 0;
+  const int rc = guarded([&] {
+    REQUIRE(h, "null handle");
+    HIPCHK(hipSetDevice(h->cfg.device));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    flag = x3_range_read(s);
+    if (reset) x3_range_reset(s);
+    HIPCHK(hipStreamSynchronize(s));
+  });
+  return rc != 0 ? rc : flag;
 }
 
 int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out, double* flops_out) {
@@ -1350,8 +1413,9 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     const int c1 = h->cfg.fea_ch, c0 = h->cfg.channels - c1;
     View x0 = h->alloc_cf(B, c0, T, L, L), fup = h->alloc_cf(B, c1, T, L, L);
     View r = h->alloc_cf(B, h->cfg.dim, T, L, L);
-    HIPCHK(hipMemsetAsync(x0.p, 0, x0.numel() * 4, s));
-    HIPCHK(hipMemsetAsync(fup.p, 0, fup.numel() * 4, s));
+    // random operands (zero-filled ones run at a higher clock than real data)
+    fill_normal(s, x0.p, 1, (int)x0.numel(), 17, 0, 0, 1);
+    fill_normal(s, fup.p, 1, (int)fup.numel(), 17, 0, 0, 2);
     const PackedW& w = h->P("init_conv.weight");
     float* bias = h->D("init_conv.bias");
     h->conv(r, x0, &fup, w, 1, 3, bias);  // warm

@@ -88,15 +88,17 @@ class Unet3D(nn.Module):
         self._native = None
         self._native_version = None
         self._extra_state = {}
+        self.precision = None  # conv arithmetic ('fp32' | 'f16x3'); None = _lib.DEFAULT_PRECISION
 
     # -- native handle management --------------------------------------------
     def _state_version(self):
         return tuple((p.data_ptr(), p._version) for p in self.parameters())
 
     def native(self, timesteps_buffers, max_batch, device_index):
-        ver = (self._state_version(), id(timesteps_buffers), max_batch, device_index)
+        ver = (self._state_version(), id(timesteps_buffers), max_batch, device_index, self.precision)
         if self._native is None or self._native_version != ver:
-            h = _lib.Handle(self.ucfg, int(timesteps_buffers['betas'].shape[0]), max_batch, device_index)
+            h = _lib.Handle(self.ucfg, int(timesteps_buffers['betas'].shape[0]), max_batch, device_index,
+                            precision=self.precision)
             sd = {k: v for k, v in self.state_dict().items()}
             sd.update(timesteps_buffers)
             h.load_state(sd)

@@ -33,6 +33,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 PKG = '140-extdm-distribution-extrapolation-diffusion-model-for-video-prediction_amd'
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 matrix peak
+# f16x3: three v_mfma_f32_32x32x16_f16 per fp32 product; fp16 dense MFMA peak 2516.6 TF/s
+# (32x32x16 = 32768 FLOP per 32 cycles per SIMD, 1024 SIMDs, 2.4 GHz) / 3
+F16X3_PEAK_TFLOPS = 2516.6 / 3
 
 
 def parse():
@@ -47,6 +50,8 @@ def parse():
     ap.add_argument('--tp', type=int, default=14)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=4)
+    ap.add_argument('--precision', default=None, choices=['fp32', 'f16x3'],
+                    help='conv arithmetic (include/extdm.h EXTDM_PRECISION_*); default: the package default')
     return ap.parse_args()
 
 
@@ -112,6 +117,8 @@ def main():
                                 estimate_occlusion_map=False)
     fd = pkg.FlowDiffusion(config=cfg, is_train=False, Unet3D_architecture=unet_arch, wrapper=wrapper).to(dev)
     fd.diffusion.max_batch = B
+    precision = args.precision or pkg._lib.DEFAULT_PRECISION
+    fd.unet.precision = precision
     tc, tp = fd.cond_frame_num, fd.pred_frame_num
     rounds = -(-args.total_pred // tp)
     clips = synthetic_clips(B, tc, 64, 1234 + rank).to(dev)
@@ -151,12 +158,16 @@ def main():
         assert torch.isfinite(out).all()
         ms_layer, flops = h.bench_layer(B, 0, 20)
         achieved = flops / (ms_layer * 1e-3) / 1e12
+        if precision == 'f16x3':
+            kname, peak = 'conv_x3_kernel<7,64,256,1,4> (init_conv 512->64, 1x7x7, f16x3)', F16X3_PEAK_TFLOPS
+        else:
+            kname, peak = 'conv_halo_kernel<7,64,1,128> (init_conv 512->64, 1x7x7, fp32 MFMA)', FP32_MFMA_PEAK_TFLOPS
         traffic = None
         pmc = os.path.join(REPO, 'profiles', 'pmc_init_conv.json')
         if os.path.exists(pmc):
             try:
                 j = json.load(open(pmc))
-                if int(j.get('batch', -1)) == B:
+                if int(j.get('batch', -1)) == B and j.get('precision', 'fp32') == precision:
                     traffic = j.get('hbm_bytes_per_launch')
             except (ValueError, OSError):
                 traffic = None
@@ -165,7 +176,8 @@ def main():
         result = {
             'metric': meta['metric'], 'value': round(value, 4), 'unit': 'frames/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 2),
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32',
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': 'fp32' if precision == 'fp32' else 'fp32 (f16x3 split-MFMA convs, fp32 accumulate)',
             'data': 'synthetic (U[0,1) PCG64 clips, seeded random-init weights; no dataset/checkpoint offline)',
             'config': {'workload': f'BAIR 64x64 ch3 {tc}->{args.total_pred} (tp={tp} x {rounds} rounds), '
                                    f'{sampler} steps, u12 Unet3D dim 64 mults (1,2,4,4), LFAE encoder + '
@@ -173,9 +185,8 @@ def main():
                        'global_batch': world * B, 'batch_per_gpu': B, 'sampling_steps': S_steps,
                        'rounds': rounds, 'parallelism': f'clip-shard x{world} (+RCCL all-gather)',
                        'workspace_gb': round(h.workspace_bytes() / 2 ** 30, 2)},
-            'roofline': {'bound': 'mfma', 'kernel': 'conv_halo_kernel<7,64,1> (init_conv 512->64, 1x7x7)',
-                         'achieved': round(achieved, 2), 'peak': FP32_MFMA_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                         'frac': round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), 'traffic': traffic},
+            'roofline': {'bound': 'mfma', 'kernel': kname, 'achieved': round(achieved, 2), 'peak': round(peak, 1),
+                         'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4), 'traffic': traffic},
         }
         if not args.no_cpu_baseline and world == 1:
             result['cpu_baseline'] = cpu_baseline(pkg, fd, rounds, 1000, args.cpu_steps)

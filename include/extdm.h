@@ -47,6 +47,13 @@ typedef struct ExtdmHandle ExtdmHandle;
  *            cond_fea at latent resolution, fea: [B,fea_ch,tc-1+tp,L,L]) */
 enum { EXTDM_ARCH_U12 = 0, EXTDM_ARCH_ADA = 1, EXTDM_ARCH_ADA_U22 = 2, EXTDM_ARCH_WO_REF = 3 };
 enum { EXTDM_SAMPLER_DDPM = 0, EXTDM_SAMPLER_DDIM = 1 };
+/* Arithmetic of the direct convolutions (every tensor stays fp32):
+ *   FP32   v_mfma_f32_32x32x2_f32 (exact fp32 products and sums)
+ *   F16X3  fp32 operands split as hi + lo fp16 pairs, three fp16 MFMAs per product
+ *          (lo*hi + hi*lo + hi*hi) into fp32 accumulators: fp32-level error, 5.3x
+ *          the fp32 MFMA rate. Needs |activation| < 65504 at conv inputs; a value
+ *          outside raises the range flag (extdm_range_flag; extdm_sample fails). */
+enum { EXTDM_PRECISION_FP32 = 0, EXTDM_PRECISION_F16X3 = 1 };
 
 typedef struct ExtdmConfig {
   int arch;            /* EXTDM_ARCH_* */
@@ -66,6 +73,7 @@ typedef struct ExtdmConfig {
   int device;          /* HIP device ordinal */
   /* LFAE Generator decoder (flow_params.generator_params); image = frame size */
   int image, num_channels, gen_block_expansion, gen_max_features, gen_num_down_blocks, gen_num_bottleneck_blocks;
+  int precision;       /* EXTDM_PRECISION_* */
 } ExtdmConfig;
 
 int extdm_create(const ExtdmConfig* cfg, ExtdmHandle** out);
@@ -105,6 +113,11 @@ int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, fl
  * conv) with HIP events on the handle's stream; returns the average ms per
  * launch and the algorithmic FLOPs per launch. */
 int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out, double* flops_out);
+
+/* The F16X3 activation-range flag: returns 1 if any conv input since the last
+ * reset had |v| >= 65504 (results computed meanwhile are not fp32-accurate), 0 if
+ * not, <0 on error; reset != 0 clears it. Synchronises `stream`. */
+int extdm_range_flag(ExtdmHandle* h, int reset, void* stream);
 
 /* LFAE decoder (Generator.forward_with_flow) for B clips x T frames.
  * ref: [B,C,S,S] source image; flow: [B,2,T,fh,fw] (x, y grid); occ: [B,1,T,fh,fw]

@@ -1,0 +1,140 @@
+"""GPU: the f16x3 split-precision conv path (include/extdm.h EXTDM_PRECISION_F16X3).
+
+Claim under test: splitting every fp32 conv operand into an fp16 hi + lo pair and
+summing lo*hi + hi*lo + hi*hi in fp32 accumulators is as accurate as fp32
+arithmetic. Checked three ways on the same seeded inputs:
+  (1) eps against the reference golden vectors at the fp32 bar (max-abs <= 1e-4);
+  (2) eps against an fp64 evaluation of the oracle: the f16x3 error is within
+      2x the error of the fp32 CPU oracle itself (and of the fp32-MFMA path);
+  (3) sampling chains (DDPM-10 / DDIM-10, injected noise) against the golden chains.
+The activation-range guard (|v| >= 65504 at a conv input) is checked to trip.
+"""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_inputs import CONFIGS, PKG, VARIANTS, GOLDEN_BATCH, make_sd, unet_inputs
+from tests.test_oracle_golden import load
+
+pytestmark = pytest.mark.gpu
+
+pkg = importlib.import_module(PKG)
+DEV = torch.device('cuda:0')
+_H = {}
+
+
+def handle(name, precision, max_batch=4, timesteps=1000):
+    key = (name, precision, max_batch, timesteps)
+    if key not in _H:
+        cfg = CONFIGS[name]
+        h = pkg._lib.Handle(cfg, timesteps, max_batch, 0, precision=precision)
+        sd = make_sd(cfg)
+        sd.update(pkg.schedule_buffers(timesteps))
+        h.load_state(sd)
+        h.finalize()
+        _H[key] = h
+    return _H[key]
+
+
+def gpu_eps(h, x, t, cond, fea):
+    out = torch.empty(x.shape, device=DEV)
+    h.unet_forward(x.to(DEV), t.to(DEV), cond.to(DEV), fea.to(DEV), out)
+    torch.cuda.synchronize()
+    return out.cpu()
+
+
+@pytest.mark.parametrize('precision', ['f16x3', 'fp32'])
+@pytest.mark.parametrize('name', ['small', 'bair'] + VARIANTS)
+def test_unet_vs_reference_golden_both_precisions(name, precision):
+    cfg = CONFIGS[name]
+    B = GOLDEN_BATCH.get(name, 2)
+    x, t, cond, fea = unet_inputs(cfg, B=B)
+    h = handle(name, precision, max_batch=B)
+    h.range_flag(reset=True)
+    eps = gpu_eps(h, x, t, cond, fea)
+    assert h.range_flag() == 0
+    g = load(f'unet_{name}.npz')['eps']
+    err = np.abs(eps.numpy() - g).max()
+    bar = 1e-4 if name in ('small', 'bair') else 2e-4
+    assert err <= bar, err
+
+
+def _fp64_eps(cfg, x, t, cond, fea):
+    import types
+    import torch.nn.functional as F
+    from oracle import extdm_oracle as O
+    sd = {k: (v.double() if v.is_floating_point() else v) for k, v in make_sd(cfg).items()}
+    F64 = types.SimpleNamespace(**{k: getattr(F, k) for k in dir(F) if not k.startswith('__')})
+    F64.linear = lambda i, w, b=None: F.linear(i.to(w.dtype), w, b)
+    saved = O.F
+    O.F = F64
+    try:
+        with torch.no_grad():
+            return O.unet_forward(sd, cfg.as_dict(), x.double(), t, cond.double(), fea.double())
+    finally:
+        O.F = saved
+
+
+def test_f16x3_error_vs_fp64_matches_fp32():
+    """BAIR Unet3D at B=1: error against fp64 of (a) the fp32 CPU oracle, (b) the
+    fp32-MFMA path, (c) the f16x3 path. (c) must stay within 2x of (a) in rms and max."""
+    from oracle import extdm_oracle as O
+    cfg = CONFIGS['bair']
+    x, t, cond, fea = unet_inputs(cfg, B=1)
+    ref = _fp64_eps(cfg, x, t, cond, fea)
+    with torch.no_grad():
+        cpu32 = O.unet_forward(make_sd(cfg), cfg.as_dict(), x, t, cond, fea).double()
+    g32 = gpu_eps(handle('bair', 'fp32', max_batch=1), x, t, cond, fea).double()
+    g3 = gpu_eps(handle('bair', 'f16x3', max_batch=1), x, t, cond, fea).double()
+
+    def stats(e):
+        d = e - ref
+        return d.abs().max().item(), d.pow(2).mean().sqrt().item()
+
+    (m_cpu, r_cpu), (m_32, r_32), (m_3, r_3) = stats(cpu32), stats(g32), stats(g3)
+    print(f'vs fp64: cpu-fp32 max {m_cpu:.3e} rms {r_cpu:.3e} | gpu-fp32 max {m_32:.3e} rms {r_32:.3e} | '
+          f'gpu-f16x3 max {m_3:.3e} rms {r_3:.3e}')
+    assert r_3 <= 2.0 * r_cpu and m_3 <= 2.0 * m_cpu, (r_3, r_cpu, m_3, m_cpu)
+
+
+def test_f16x3_ddpm10_and_ddim10_chains_vs_reference_golden():
+    """Same fixtures and noise streams as test_gpu_parity's fp32 chain tests."""
+    cfg = CONFIGS['small']
+    x, _, cond, fea = unet_inputs(cfg)
+    g = load('sampler_small.npz')
+    h10 = handle('small', 'f16x3', max_batch=2, timesteps=10)
+    torch.manual_seed(7)
+    xT = torch.randn(x.shape)
+    noises = torch.stack([torch.randn(x.shape) for _ in range(10)])
+    out = torch.empty(x.shape, device=DEV)
+    h10.sample(0, list(range(9, -1, -1)), None, 0., cond.to(DEV), fea.to(DEV), out, x_T=xT.to(DEV),
+               noise=noises.to(DEV).contiguous())
+    torch.cuda.synchronize()
+    err = np.abs(out.cpu().numpy() - g['ddpm10']).max()
+    assert err <= 2e-4, err
+
+    h = handle('small', 'f16x3')
+    pairs = pkg.ddim_time_pairs(1000, 10)
+    torch.manual_seed(11)
+    xT = torch.randn(x.shape)
+    noises = torch.stack([torch.randn(x.shape) for _ in range(10)])
+    out = torch.empty(x.shape, device=DEV)
+    h.sample(1, [p[0] for p in pairs], [p[1] for p in pairs], 1.0, cond.to(DEV), fea.to(DEV), out, x_T=xT.to(DEV),
+             noise=noises.to(DEV).contiguous())
+    torch.cuda.synchronize()
+    err = np.abs(out.cpu().numpy() - g['ddim10']).max()
+    assert err <= 2e-4, err
+
+
+def test_f16x3_range_guard_trips():
+    """init_conv (a split conv) reads the cond features directly: scale them out of range."""
+    cfg = CONFIGS['bair']
+    x, t, cond, fea = unet_inputs(cfg, B=1)
+    h = handle('bair', 'f16x3', max_batch=1)
+    h.range_flag(reset=True)
+    gpu_eps(h, x, t, cond, fea * 1e5)
+    assert h.range_flag(reset=True) == 1
+    gpu_eps(h, x, t, cond, fea)
+    assert h.range_flag() == 0
