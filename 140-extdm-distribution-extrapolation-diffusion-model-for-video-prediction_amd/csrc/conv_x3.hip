@@ -24,6 +24,7 @@
 // buffered; the next channel block's input is prefetched into registers while
 // the KS ky-iterations of the current one run.
 #include <algorithm>
+#include <cstdlib>
 
 #include "kernels.h"
 
@@ -62,27 +63,30 @@ template <> struct XMaxX3<7, 256> { static constexpr int v = 560; };
 template <> struct XMaxX3<3, 256> { static constexpr int v = 576; };
 template <> struct XMaxX3<3, 128> { static constexpr int v = 288; };
 template <> struct XMaxX3<1, 128> { static constexpr int v = 128; };
+template <> struct XMaxX3<7, 512> { static constexpr int v = 836; };
+template <> struct XMaxX3<3, 512> { static constexpr int v = 800; };
 
-template <int KS, int BM, int BN, int NG, int WN>
-__global__ __launch_bounds__(256) void conv_x3_kernel(X3Args a) {
+template <int KS, int BM, int BN, int NG, int WN, int NW, int XBUF>
+__global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
+  constexpr int NT = NW * 64;
   constexpr int PAD = KS / 2;
   constexpr int CIB = 16 * NG;
   constexpr int MT32 = BM / 32;
   constexpr int STEPS = NG * KS;                // per A slot: (g, kx)
   constexpr int AH = STEPS * MT32 * 2 * 512;    // halves per A slot
   constexpr int XMAX = XMaxX3<KS, BN>::v;
-  constexpr int NSLOT = (XMAX * NG + 255) / 256;
-  constexpr int WM = 4 / WN;
+  constexpr int NSLOT = (XMAX * NG + NT - 1) / NT;
+  constexpr int WM = NW / WN;
   constexpr int TM = BM / (32 * WM);
   constexpr int TN = BN / (32 * WN);
-  static_assert(TM >= 1 && TN >= 1 && WM * WN == 4, "bad tile");
+  static_assert(TM >= 1 && TN >= 1 && WM * WN == NW, "bad tile");
 
   extern __shared__ __attribute__((aligned(16))) _Float16 smx[];
   const int XH = a.XPOS * NG * 32;  // halves per X slot (hi + lo)
   _Float16* As0 = smx;
   _Float16* As1 = smx + AH;
   _Float16* Xs0 = smx + 2 * AH;
-  _Float16* Xs1 = Xs0 + XH;
+  _Float16* Xs1 = XBUF == 2 ? Xs0 + XH : Xs0;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -96,12 +100,12 @@ __global__ __launch_bounds__(256) void conv_x3_kernel(X3Args a) {
   const _Float16* wt = a.w + (long)mtile * NIT * AH;
 
   // ---- staging slots: (group, halo position), 16 channels each ----
-  int sg[NSLOT], spos[NSLOT], soff[NSLOT];
-  long sb0[NSLOT], sb1[NSLOT];
+  // The host guarantees C0 % 16 == 0, so a 16-channel group lies in one source.
+  int sg[NSLOT], spos[NSLOT], soff0[NSLOT], soff1[NSLOT];
 #pragma unroll
   for (int j = 0; j < NSLOT; ++j) {
-    const int sl = tid + 256 * j;
-    sg[j] = -1; spos[j] = 0; soff[j] = -1; sb0[j] = 0; sb1[j] = 0;
+    const int sl = tid + NT * j;
+    sg[j] = -1; spos[j] = 0; soff0[j] = -1; soff1[j] = -1;
     if (sl < a.XPOS * NG) {
       const int g = sl / a.XPOS, pos = sl - g * a.XPOS;
       const int p = pos / (THK * a.RS);
@@ -111,10 +115,9 @@ __global__ __launch_bounds__(256) void conv_x3_kernel(X3Args a) {
       const int iy = row0 + rr - PAD, ix = cc - PAD;
       sg[j] = g; spos[j] = pos;
       if (q < a.P && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
-        soff[j] = iy * a.W + ix;
         const int b = q / a.T, t = q - b * a.T;
-        sb0[j] = (long)b * a.i0b + (long)t * a.i0t;
-        sb1[j] = (long)b * a.i1b + (long)t * a.i1t;
+        soff0[j] = (int)((long)b * a.i0b + (long)t * a.i0t) + iy * a.W + ix;
+        soff1[j] = (int)((long)b * a.i1b + (long)t * a.i1t) + iy * a.W + ix;
       }
     }
   }
@@ -124,17 +127,22 @@ __global__ __launch_bounds__(256) void conv_x3_kernel(X3Args a) {
   auto load_x = [&](int cgb) {
 #pragma unroll
     for (int j = 0; j < NSLOT; ++j) {
+      const int ci0 = cgb * CIB + sg[j] * 16;
+      const bool src1 = ci0 >= a.C0;
+      const float* base = src1 ? a.in1 + (long)(ci0 - a.C0) * a.i1c : a.in0 + (long)ci0 * a.i0c;
+      const int cs = src1 ? (int)a.i1c : (int)a.i0c;
+      const int off = src1 ? soff1[j] : soff0[j];
+      if (off >= 0 && ci0 + 16 <= a.Cin) {
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        float v = 0.f;
-        const int ci = cgb * CIB + sg[j] * 16 + c;
-        if (soff[j] >= 0 && ci < a.Cin)
-          v = ci < a.C0 ? a.in0[sb0[j] + (long)ci * a.i0c + soff[j]]
-                        : a.in1[sb1[j] + (long)(ci - a.C0) * a.i1c + soff[j]];
-        xr[j][c] = v;
+        for (int c = 0; c < 16; ++c) xr[j][c] = base[off + c * cs];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) xr[j][c] = (off >= 0 && ci0 + c < a.Cin) ? base[off + c * cs] : 0.f;
       }
     }
   };
+  // 16-byte chunk h of position pos sits at chunk h ^ bit3(pos): conflict-free
+  // ds_read_b128 for 32 consecutive positions (lane groups of 16, MI355X_MICROARCH §LDS)
   auto store_x = [&](_Float16* Xs) {
 #pragma unroll
     for (int j = 0; j < NSLOT; ++j) {
@@ -149,18 +157,20 @@ __global__ __launch_bounds__(256) void conv_x3_kernel(X3Args a) {
         lo0[c] = (_Float16)(v0 - (float)a0);
         lo1[c] = (_Float16)(v1 - (float)a1);
       }
+      const int sw = (spos[j] >> 3) & 1;
       _Float16* dh = Xs + ((long)sg[j] * a.XPOS + spos[j]) * 16;
       _Float16* dl = dh + (long)NG * a.XPOS * 16;
-      *reinterpret_cast<h8*>(dh) = hi0;
-      *reinterpret_cast<h8*>(dh + 8) = hi1;
-      *reinterpret_cast<h8*>(dl) = lo0;
-      *reinterpret_cast<h8*>(dl + 8) = lo1;
+      *reinterpret_cast<h8*>(dh + 8 * sw) = hi0;
+      *reinterpret_cast<h8*>(dh + 8 * (sw ^ 1)) = hi1;
+      *reinterpret_cast<h8*>(dl + 8 * sw) = lo0;
+      *reinterpret_cast<h8*>(dl + 8 * (sw ^ 1)) = lo1;
     }
   };
   constexpr int NPIECE = AH / 512;  // 1 KiB pieces
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   auto load_a = [&](int it, _Float16* As) {
     const _Float16* src = wt + (long)it * AH;
-    for (int pc = wave; pc < NPIECE; pc += 4)
+    for (int pc = wave_u; pc < NPIECE; pc += NW)
       __builtin_amdgcn_global_load_lds((const void*)(src + pc * 512 + lane * 8), (lds_ptr_t)(As + pc * 512), 16, 0,
                                        0);
   };
@@ -210,7 +220,7 @@ __global__ __launch_bounds__(256) void conv_x3_kernel(X3Args a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int pos = bpos[j] + ky * a.RS + kx;
-          const _Float16* bp = Xs + ((long)g * a.XPOS + pos) * 16 + h * 8;
+          const _Float16* bp = Xs + ((long)g * a.XPOS + pos) * 16 + 8 * (h ^ ((pos >> 3) & 1));
           bh[j] = *reinterpret_cast<const h8*>(bp);
           bl[j] = *reinterpret_cast<const h8*>(bp + (long)NG * a.XPOS * 16);
         }
@@ -224,7 +234,10 @@ __global__ __launch_bounds__(256) void conv_x3_kernel(X3Args a) {
           }
       }
     }
-    if (ky == KS - 1 && cgb + 1 < a.ncgb) store_x((cgb & 1) ? Xs0 : Xs1);
+    if (ky == KS - 1 && cgb + 1 < a.ncgb) {
+      if (XBUF == 1) __syncthreads();  // single X buffer: every wave is done with it
+      store_x((cgb & 1) ? Xs0 : Xs1);
+    }
     __syncthreads();
   }
   if (range_bad) atomicOr(&g_x3_range, 1);
@@ -262,25 +275,26 @@ __global__ __launch_bounds__(256) void conv_x3_kernel(X3Args a) {
   }
 }
 
-template <int KS, int BM, int BN, int NG, int WN>
+template <int KS, int BM, int BN, int NG, int WN, int NW, int XBUF>
 void launch(hipStream_t s, const X3Args& a, unsigned ntiles) {
   constexpr int AH = NG * KS * (BM / 32) * 2 * 512;
-  const size_t lds = ((size_t)2 * AH + (size_t)2 * a.XPOS * NG * 32) * sizeof(_Float16);
+  const size_t lds = ((size_t)2 * AH + (size_t)XBUF * a.XPOS * NG * 32) * sizeof(_Float16);
   dim3 grid(ntiles, (a.Cout + BM - 1) / BM);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, BM, BN, NG, WN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, BM, BN, NG, WN, NW, XBUF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_x3_kernel<KS, BM, BN, NG, WN>), grid, dim3(256), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<KS, BM, BN, NG, WN, NW, XBUF>), grid, dim3(NW * 64), lds, s, a);
 }
 
 }  // namespace
 
 X3Tile x3_tile(int ks, int cout) {
   X3Tile t{};
-  if (ks == 7) { t.bm = 64; t.bn = 256; t.ng = 1; }
+  // 7x7 (init_conv): 16 waves over 64 x 512 px tiles, one X buffer; 3x3: 8 waves
+  if (ks == 7) { t.bm = 64; t.bn = 512; t.ng = 1; }
   else if (ks == 3) { if (cout <= 64) { t.bm = 64; t.bn = 256; } else { t.bm = 128; t.bn = 128; } t.ng = 1; }
   else if (ks == 1) { t.bm = cout <= 64 ? 64 : 128; t.bn = 128; t.ng = 2; }
   return t;
@@ -293,13 +307,16 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   const int H = in0.H, W = in0.W;
   const X3Tile tl{w.xbm, w.xbn, w.xng};
   if (out.H != H || out.W != W || W > tl.bn || tl.bn % W != 0) return false;
+  if (in1 && in0.C % 16 != 0) return false;  // a 16-channel group must not straddle the two sources
+  // 32-bit in-plane offsets in the staging
+  if ((long)in0.B * in0.sb > (1L << 31) || (in1 && (long)in1->B * in1->sb > (1L << 31))) return false;
   X3Args a{};
   a.TH = std::min(H, tl.bn / W);
   if (tl.bn % (a.TH * W) != 0) return false;
   a.NP = tl.bn / (a.TH * W);
   a.RS = W + ks - 1;
   a.XPOS = a.NP * (a.TH + ks - 1) * a.RS;
-  const int xmax = ks == 7 ? 560 : (ks == 3 ? (tl.bn == 256 ? 576 : 288) : 128);
+  const int xmax = tl.bn == 512 ? (ks == 7 ? 836 : 800) : (ks == 7 ? 560 : (ks == 3 ? (tl.bn == 256 ? 576 : 288) : 128));
   if (a.XPOS > xmax) return false;
   a.in0 = in0.p; a.i0b = in0.sb; a.i0c = in0.sc; a.i0t = in0.st; a.C0 = in0.C;
   if (in1) { a.in1 = in1->p; a.i1b = in1->sb; a.i1c = in1->sc; a.i1t = in1->st; a.Cin = in0.C + in1->C; }
@@ -310,11 +327,17 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   a.nrow_tiles = (H + a.TH - 1) / a.TH;
   a.e = epi;
   const unsigned ntiles = (unsigned)(((a.P + a.NP - 1) / a.NP) * a.nrow_tiles);
-  if (ks == 7 && tl.bm == 64) launch<7, 64, 256, 1, 4>(s, a, ntiles);
-  else if (ks == 3 && tl.bm == 64) launch<3, 64, 256, 1, 4>(s, a, ntiles);
-  else if (ks == 3 && tl.bm == 128) launch<3, 128, 128, 1, 2>(s, a, ntiles);
-  else if (ks == 1 && tl.bm == 64) launch<1, 64, 128, 2, 4>(s, a, ntiles);
-  else if (ks == 1 && tl.bm == 128) launch<1, 128, 128, 2, 2>(s, a, ntiles);
+  if (tl.bn == 512) {
+    if (ks == 7 && tl.bm == 64) launch<7, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
+    else if (ks == 3 && tl.bm == 64) launch<3, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
+    else return false;
+    return true;
+  }
+  if (ks == 7 && tl.bm == 64) launch<7, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
+  else if (ks == 3 && tl.bm == 64) launch<3, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
+  else if (ks == 3 && tl.bm == 128) launch<3, 128, 128, 1, 2, 8, 2>(s, a, ntiles);
+  else if (ks == 1 && tl.bm == 64) launch<1, 64, 128, 2, 4, 4, 2>(s, a, ntiles);
+  else if (ks == 1 && tl.bm == 128) launch<1, 128, 128, 2, 2, 4, 2>(s, a, ntiles);
   else return false;
   return true;
 }

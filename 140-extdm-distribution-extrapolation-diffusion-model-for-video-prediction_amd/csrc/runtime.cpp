@@ -1408,22 +1408,34 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     Scope sc(h->arena);
     const int T = h->frames(), L = h->cfg.latent;
     // layer 0: init_conv, conv3d (1,7,7) channels -> dim over (B, T, L, L) (u12:913, 1041),
-    // input as the forward issues it: two sources (x-branch, cond_fea branch)
-    REQUIRE(layer == 0, "unknown layer id");
-    const int c1 = h->cfg.fea_ch, c0 = h->cfg.channels - c1;
-    View x0 = h->alloc_cf(B, c0, T, L, L), fup = h->alloc_cf(B, c1, T, L, L);
-    View r = h->alloc_cf(B, h->cfg.dim, T, L, L);
+    // input as the forward issues it: two sources (x-branch, cond_fea branch).
+    // layers 1-4: ResnetBlock convs (u12:165, 200) at levels 0-2 and a level-0 res_conv.
+    static const char* names[] = {"init_conv.weight", "downs.0.0.block2.proj.weight", "downs.1.0.block2.proj.weight",
+                                  "downs.2.0.block2.proj.weight", "ups.3.0.res_conv.weight"};
+    static const int levels[] = {0, 0, 1, 2, 0};
+    REQUIRE(layer >= 0 && layer < 5, "unknown layer id");
+    const std::string wn = names[layer];
+    REQUIRE(h->has(wn), "bench layer weight missing: " + wn);
+    const auto& sh = h->H(wn).shape;
+    const int co = (int)sh[0], ci = (int)sh[1], ks = (int)sh.back();
+    const int Lq = L >> levels[layer];
+    const int c1 = layer == 0 ? h->cfg.fea_ch : 0, c0 = ci - c1;
+    View x0 = h->alloc_cf(B, c0, T, Lq, Lq);
+    View fup = c1 ? h->alloc_cf(B, c1, T, Lq, Lq) : x0;
+    View r = h->alloc_cf(B, co, T, Lq, Lq);
     // random operands (zero-filled ones run at a higher clock than real data)
     fill_normal(s, x0.p, 1, (int)x0.numel(), 17, 0, 0, 1);
-    fill_normal(s, fup.p, 1, (int)fup.numel(), 17, 0, 0, 2);
-    const PackedW& w = h->P("init_conv.weight");
-    float* bias = h->D("init_conv.bias");
-    h->conv(r, x0, &fup, w, 1, 3, bias);  // warm
+    if (c1) fill_normal(s, fup.p, 1, (int)fup.numel(), 17, 0, 0, 2);
+    const PackedW& w = h->P(wn);
+    const std::string bn = wn.substr(0, wn.size() - 6) + "bias";
+    float* bias = h->has(bn) ? h->D(bn) : nullptr;
+    const View* in1 = c1 ? &fup : nullptr;
+    h->conv(r, x0, in1, w, 1, ks / 2, bias);  // warm
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     HIPCHK(hipEventRecord(a, s));
-    for (int i = 0; i < iters; ++i) h->conv(r, x0, &fup, w, 1, 3, bias);
+    for (int i = 0; i < iters; ++i) h->conv(r, x0, in1, w, 1, ks / 2, bias);
     HIPCHK(hipEventRecord(b, s));
     HIPCHK(hipEventSynchronize(b));
     float ms = 0.f;
@@ -1431,7 +1443,7 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     (void)hipEventDestroy(a);
     (void)hipEventDestroy(b);
     *ms_out = ms / iters;
-    *flops_out = 2.0 * B * T * L * L * (double)h->cfg.dim * h->cfg.channels * 49.0;
+    *flops_out = 2.0 * B * T * Lq * Lq * (double)co * ci * ks * ks;
   });
 }
 

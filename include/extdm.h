@@ -108,10 +108,12 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
 int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, float eta, float* x, const float* eps,
                        const float* noise, float* thresh_out, void* stream);
 
-/* Measurement hook for bench.py: time `iters` launches of one hot-path kernel
- * exactly as the forward issues it (layer 0 = init_conv, the (1,7,7) 512->dim
- * conv) with HIP events on the handle's stream; returns the average ms per
- * launch and the algorithmic FLOPs per launch. */
+/* Measurement hook for bench.py: time `iters` launches of one hot-path conv
+ * exactly as the forward issues it, on random operands, with HIP events on the
+ * handle's stream; returns the average ms per launch and the algorithmic FLOPs
+ * per launch. layer 0 = init_conv (1,7,7) channels->dim (two sources); 1, 2, 3 =
+ * ResnetBlock (1,3,3) convs at levels 0, 1, 2 (downs.{0,1,2}.0.block2); 4 = the
+ * level-0 up ResnetBlock's 1x1 res_conv (ups.3.0.res_conv). */
 int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out, double* flops_out);
 
 /* The F16X3 activation-range flag: returns 1 if any conv input since the last
