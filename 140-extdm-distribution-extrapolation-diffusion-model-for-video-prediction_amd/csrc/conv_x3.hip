@@ -100,7 +100,6 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   const _Float16* wt = a.w + (long)mtile * NIT * AH;
 
   // ---- staging slots: (group, halo position), 16 channels each ----
-  // The host guarantees C0 % 16 == 0, so a 16-channel group lies in one source.
   int sg[NSLOT], spos[NSLOT], soff0[NSLOT], soff1[NSLOT];
 #pragma unroll
   for (int j = 0; j < NSLOT; ++j) {
@@ -132,12 +131,20 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
       const float* base = src1 ? a.in1 + (long)(ci0 - a.C0) * a.i1c : a.in0 + (long)ci0 * a.i0c;
       const int cs = src1 ? (int)a.i1c : (int)a.i0c;
       const int off = src1 ? soff1[j] : soff0[j];
-      if (off >= 0 && ci0 + 16 <= a.Cin) {
+      const int cend = src1 ? a.Cin : a.C0;  // the group's source ends here
+      if (off >= 0 && ci0 + 16 <= cend) {
 #pragma unroll
         for (int c = 0; c < 16; ++c) xr[j][c] = base[off + c * cs];
       } else {
+        // ragged group: the tail of a source (and the start of in1 when C0 % 16 != 0)
 #pragma unroll
-        for (int c = 0; c < 16; ++c) xr[j][c] = (off >= 0 && ci0 + c < a.Cin) ? base[off + c * cs] : 0.f;
+        for (int c = 0; c < 16; ++c) {
+          const int ci = ci0 + c;
+          float v = 0.f;
+          if (soff0[j] >= 0 && ci < a.Cin)
+            v = ci < a.C0 ? a.in0[(long)ci * a.i0c + soff0[j]] : a.in1[(long)(ci - a.C0) * a.i1c + soff1[j]];
+          xr[j][c] = v;
+        }
       }
     }
   };
@@ -307,7 +314,6 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   const int H = in0.H, W = in0.W;
   const X3Tile tl{w.xbm, w.xbn, w.xng};
   if (out.H != H || out.W != W || W > tl.bn || tl.bn % W != 0) return false;
-  if (in1 && in0.C % 16 != 0) return false;  // a 16-channel group must not straddle the two sources
   // 32-bit in-plane offsets in the staging
   if ((long)in0.B * in0.sb > (1L << 31) || (in1 && (long)in1->B * in1->sb > (1L << 31))) return false;
   X3Args a{};

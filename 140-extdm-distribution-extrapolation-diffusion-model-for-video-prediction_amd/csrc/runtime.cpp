@@ -308,6 +308,10 @@ struct ExtdmHandle {
     REQUIRE((in1 ? in0.C + in1->C : in0.C) * w.KH * w.KW == w.K || w.mode == MODE_DECONV,
             "conv: input channels do not match the weight");
     REQUIRE(out.C == w.M, "conv: output channels do not match the weight");
+    REQUIRE(in0.B == out.B && (!in1 || in1->B == out.B) && (!res || res->B == out.B),
+            "conv: batch of an operand does not match the output");
+    REQUIRE(w.mode != MODE_CONV || stride != 1 || (in0.T == out.T && (!in1 || in1->T == out.T)),
+            "conv: frame count of an operand does not match the output");
     if (plan) return;
     ConvEpi e;
     e.bias = bias;
@@ -528,24 +532,93 @@ struct ExtdmHandle {
   }
 
   // TrajWarp (u12:804-827) -> the fused pred-frame features fp' [B,256,tp,fs,fs]
-  void trajwarp(const View& x0, const View& fea, const View& fp_out) {
-    Scope sc(arena);
-    const int B = x0.B, C = fea.C, tc = cfg.tc, tp = cfg.tp, fs = cfg.fea_size;
-    REQUIRE(x0.H / 2 == fs && x0.W / 2 == fs, "TrajWarp: maxpooled latent must match cond_fea size");
-    View xq = alloc_cf(B, x0.C, tp, fs, fs);
-    if (!plan) maxpool_hw2(s, xq, x0.frames(tc, tp));
+  // TrajWarp (u12:719-827) in two halves. The k / v projections of the cond-frame
+  // features fm = cond_fea[:, :, :tc] depend only on cond_fea: trajwarp_kv runs once
+  // per sampling call into the handle's cond cache. trajwarp_q takes x0p, the
+  // init_noise_conv output of the tp predicted frames.
+  void trajwarp_kv(const View& fea) {
     const std::string c = "init_traj.cross_att";
-    View q = alloc_cf(B, C, tp, fs, fs), k = alloc_cf(B, C, tc, fs, fs), v = alloc_cf(B, C, tc, fs, fs);
+    View fm = fea.frames(0, cfg.tc);
+    conv(with_batch(kv_k, fea.B), fm, nullptr, P(c + ".linear_k.weight"), 1, 0, D(c + ".linear_k.bias"), nullptr,
+         ACT_RELU);
+    conv(with_batch(kv_v, fea.B), fm, nullptr, P(c + ".linear_v.weight"), 1, 0, D(c + ".linear_v.bias"), nullptr,
+         ACT_RELU);
+  }
+  void trajwarp_q(const View& x0p, const View& fea, const View& fp_out) {
+    Scope sc(arena);
+    const int B = x0p.B, C = fea.C, tc = cfg.tc, tp = cfg.tp, fs = cfg.fea_size;
+    REQUIRE(x0p.H / 2 == fs && x0p.W / 2 == fs, "TrajWarp: maxpooled latent must match cond_fea size");
+    View xq = alloc_cf(B, x0p.C, tp, fs, fs);
+    if (!plan) maxpool_hw2(s, xq, x0p);
+    const std::string c = "init_traj.cross_att";
+    View q = alloc_cf(B, C, tp, fs, fs);
     conv(q, xq, nullptr, P(c + ".linear_q.weight"), 1, 0, D(c + ".linear_q.bias"), nullptr, ACT_RELU);
-    View fm = fea.frames(0, tc);
-    conv(k, fm, nullptr, P(c + ".linear_k.weight"), 1, 0, D(c + ".linear_k.bias"), nullptr, ACT_RELU);
-    conv(v, fm, nullptr, P(c + ".linear_v.weight"), 1, 0, D(c + ".linear_v.bias"), nullptr, ACT_RELU);
     View a = alloc_cf(B, C, tp, fs, fs);
-    if (!plan) cross_attention(s, q.p, k.p, v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
+    if (!plan) cross_attention(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
     View fm2p = alloc_cf(B, C, tp, fs, fs);
     conv(fm2p, a, nullptr, P(c + ".linear_o.weight"), 1, 0, D(c + ".linear_o.bias"), nullptr, ACT_RELU);
     View fp = fea.frames(tc, tp);
     conv(fp_out, fp, &fm2p, P("init_traj.fuser.weight"), 1, 0, D("init_traj.fuser.bias"));
+  }
+
+  // Cond cache (filled by prepare_cond, read by unet_step): the init_conv output of the
+  // tm conditioning frames (every op up to init_conv is per frame, u12:1029-1041, and
+  // TrajWarp passes fm = cond_fea[:, :, :tc] through unchanged, u12:792), TrajWarp's
+  // k / v of fm, and for ada / ada_u22 the resized cond_adaptor + cond_temporal_attn
+  // features (ada.py:1035-1036), which depend on cond_fea only.
+  View r_all, kv_k, kv_v, fup_all;
+  void alloc_cond_cache() {
+    const int Bm = cfg.max_batch, T = frames(), L = cfg.latent, fs = cfg.fea_size;
+    r_all = cf_view(dmalloc((size_t)Bm * cfg.dim * T * L * L * 4), Bm, cfg.dim, T, L, L);
+    if (cfg.arch == EXTDM_ARCH_U12) {
+      kv_k = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * cfg.tc * fs * fs * 4), Bm, cfg.fea_ch, cfg.tc, fs, fs);
+      kv_v = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * cfg.tc * fs * fs * 4), Bm, cfg.fea_ch, cfg.tc, fs, fs);
+    }
+    if (cfg.arch == EXTDM_ARCH_ADA || cfg.arch == EXTDM_ARCH_ADA_U22)
+      fup_all = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * T * L * L * 4), Bm, cfg.fea_ch, T, L, L);
+  }
+  static View with_batch(View v, int B) { v.B = B; return v; }
+
+  void prepare_cond(int B, const float* cond, const float* fea) {
+    Scope top(arena);
+    const int arch = cfg.arch;
+    const int tc = tm(), T = frames(), L = cfg.latent, fs = cfg.fea_size;
+    View vc = cf_view(const_cast<float*>(cond), B, 3, cfg.tc, L, L);
+    View vf = cf_view(const_cast<float*>(fea), B, cfg.fea_ch, T, fs, fs);
+    View r = with_batch(r_all, B).frames(0, tc);
+    if (arch == EXTDM_ARCH_WO_REF) {
+      // cat(cond_frames[:, :, :-1], x) ++ cond_fea at latent resolution (wo_ref.py:911-921)
+      REQUIRE(fs == L, "wo_ref: cond_fea must be at the latent resolution");
+      const View fc = vf.frames(0, tc);
+      conv(r, vc.frames(0, tc), &fc, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+      return;
+    }
+    View fup;
+    if (arch == EXTDM_ARCH_U12) {
+      trajwarp_kv(vf);
+      fup = alloc_cf(B, cfg.fea_ch, tc, L, L);
+      if (!plan) bilinear_frames(s, fup, vf.frames(0, tc), vf.frames(0, tc), tc);
+    } else {
+      View fa = alloc_cf(B, cfg.fea_ch, T, fs, fs);
+      if (!plan) copy_view(s, fa, vf);
+      adaptor("cond_adaptor", fa);
+      temporal("cond_temporal_attn", fa, fa);
+      View fu = with_batch(fup_all, B);
+      if (!plan) bilinear_frames(s, fu, fa, fa, T);
+      fup = fu.frames(0, tc);
+    }
+    if (arch == EXTDM_ARCH_ADA_U22) {  // no init_noise_conv (ada_u22.py:1180)
+      conv(r, vc, &fup, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+    } else {
+      View x0 = alloc_cf(B, 256, tc, L, L);
+      conv(x0, vc, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
+      conv(r, x0, &fup, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+    }
+  }
+
+  void unet_forward(int B, const float* x, const float* cond, const float* fea, float* eps) {
+    prepare_cond(B, cond, fea);
+    unet_step(B, x, fea, eps);
   }
 
   // Unet3D.forward for the four reference denoisers (arch switch, include/extdm.h):
@@ -555,46 +628,39 @@ struct ExtdmHandle {
   //   wo_ref   DenoiseNet_..._wo_ref_adaptor_cross_multi.py:906-967
   // x: [B,3,tp,L,L], cond: [B,3,tc,L,L], fea: [B,fea_ch,T,fs,fs] with T = tm + tp,
   // eps: [B,3,tp,L,L]; t_batch already on device.
-  void unet_forward(int B, const float* x, const float* cond, const float* fea, float* eps) {
+  // One denoiser evaluation given the cond cache (prepare_cond with the same cond / fea).
+  void unet_step(int B, const float* x, const float* fea, float* eps) {
     Scope top(arena);
     const int arch = cfg.arch;
     const int tc = tm(), tp = cfg.tp, T = frames(), L = cfg.latent, fs = cfg.fea_size, d0 = cfg.dim;
     const bool u22 = arch == EXTDM_ARCH_ADA_U22;
     View vx = cf_view(const_cast<float*>(x), B, 3, tp, L, L);
-    View vc = cf_view(const_cast<float*>(cond), B, 3, cfg.tc, L, L);
     View vf = cf_view(const_cast<float*>(fea), B, cfg.fea_ch, T, fs, fs);
     View veps = cf_view(eps, B, 3, tp, L, L);
 
-    View r = alloc_cf(B, d0, T, L, L);  // `r` (u12:1042)
+    View r = with_batch(r_all, B);  // `r` (u12:1042); frames [0, tm) from prepare_cond
     {
       Scope sc(arena);
-      // cat([cond_frames (minus the last in wo_ref), x], dim=2)
-      View xin = alloc_cf(B, 3, T, L, L);
-      if (!plan) { copy_view(s, xin.frames(0, tc), vc.frames(0, tc)); copy_view(s, xin.frames(tc, tp), vx); }
+      View rp = r.frames(tc, tp);
       if (arch == EXTDM_ARCH_WO_REF) {
-        // cond_fea enters at latent resolution, no feature branch (wo_ref.py:916-921)
-        REQUIRE(fs == L, "wo_ref: cond_fea must be at the latent resolution");
-        conv(r, xin, &vf, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+        const View fp = vf.frames(tc, tp);
+        conv(rp, vx, &fp, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+      } else if (arch == EXTDM_ARCH_ADA_U22) {
+        View fu = with_batch(fup_all, B).frames(tc, tp);
+        conv(rp, vx, &fu, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
       } else {
-        View x0 = xin;
-        if (arch != EXTDM_ARCH_ADA_U22) {
-          x0 = alloc_cf(B, 256, T, L, L);
-          conv(x0, xin, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
-        }
-        View fup = alloc_cf(B, cfg.fea_ch, T, L, L);
+        View x0p = alloc_cf(B, 256, tp, L, L);
+        conv(x0p, vx, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
+        View fu;
         if (arch == EXTDM_ARCH_U12) {
           View fp2 = alloc_cf(B, cfg.fea_ch, tp, fs, fs);
-          trajwarp(x0, vf, fp2);
-          if (!plan) bilinear_frames(s, fup, vf, fp2, tc);
+          trajwarp_q(x0p, vf, fp2);
+          fu = alloc_cf(B, cfg.fea_ch, tp, L, L);
+          if (!plan) bilinear_frames(s, fu, fp2, fp2, 0);
         } else {
-          // cond_adaptor then cond_temporal_attn on cond_fea (ada.py:1035-1036)
-          View fa = alloc_cf(B, cfg.fea_ch, T, fs, fs);
-          if (!plan) copy_view(s, fa, vf);
-          adaptor("cond_adaptor", fa);
-          temporal("cond_temporal_attn", fa, fa);
-          if (!plan) bilinear_frames(s, fup, fa, fa, T);
+          fu = with_batch(fup_all, B).frames(tc, tp);
         }
-        conv(r, x0, &fup, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+        conv(rp, x0p, &fu, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
       }
     }
     View xt = alloc_cf(B, d0, T, L, L);
@@ -1136,6 +1202,7 @@ struct ExtdmHandle {
   void finalize_workspace() {
     // pack every weight the forward touches by running it in planning mode
     const int B = cfg.max_batch;
+    if (has_unet()) alloc_cond_cache();
     plan = true;
     arena.planning = true;
     arena.top = arena.peak = 0;
@@ -1351,12 +1418,13 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     else fill_normal(s, out, B, n, seed, sample_base, round, 0x7FFFFFFF);
     HIPCHK(hipMemsetAsync(h->step_ctr, 0, sizeof(int), s));
     if (h->cfg.precision == EXTDM_PRECISION_F16X3) x3_range_reset(s);
+    h->prepare_cond(B, x_cond, cond_fea);  // t-independent cond-frame work, once per call
     int klo, khi;
     float w;
     h->quantile_ranks(n, klo, khi, w);
     auto step = [&]() {
       set_t_from_step(s, h->t_batch, B, h->coefs, h->step_ctr);
-      h->unet_forward(B, out, x_cond, cond_fea, h->eps_buf);
+      h->unet_step(B, out, cond_fea, h->eps_buf);
       sampler_step(s, out, h->eps_buf, B, n, h->coefs, h->step_ctr, noise, seed, sample_base, round, klo, khi, w,
                    nullptr);
       incr_counter(s, h->step_ctr);

@@ -159,7 +159,7 @@ def main():
         ms_layer, flops = h.bench_layer(B, 0, 20)
         achieved = flops / (ms_layer * 1e-3) / 1e12
         if precision == 'f16x3':
-            kname, peak = 'conv_x3_kernel<7,64,256,1,4> (init_conv 512->64, 1x7x7, f16x3)', F16X3_PEAK_TFLOPS
+            kname, peak = 'conv_x3_kernel<7,64,512,1,8,16,1> (init_conv 512->64, 1x7x7, f16x3)', F16X3_PEAK_TFLOPS
         else:
             kname, peak = 'conv_halo_kernel<7,64,1,128> (init_conv 512->64, 1x7x7, fp32 MFMA)', FP32_MFMA_PEAK_TFLOPS
         traffic = None
