@@ -11,7 +11,8 @@ LIB_PATH = os.path.join(HERE, 'libextdm_hip.so')
 EXPORTS = ['extdm_create', 'extdm_destroy', 'extdm_last_error', 'extdm_load_weight', 'extdm_finalize',
            'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_bench_layer',
            'extdm_decode', 'extdm_set_lfae', 'extdm_region_params', 'extdm_region_hw', 'extdm_bg_params',
-           'extdm_flow_predict', 'extdm_flow_hw', 'extdm_bottleneck', 'extdm_range_flag']
+           'extdm_flow_predict', 'extdm_flow_hw', 'extdm_bottleneck', 'extdm_range_flag',
+           'extdm_attn_layer']
 
 BG_TYPES = {'zero': 0, 'shift': 1, 'affine': 2, 'perspective': 3}
 
@@ -21,7 +22,6 @@ SAMPLER_DDIM = 1
 # include/extdm.h EXTDM_PRECISION_*: arithmetic of the direct convolutions
 PRECISIONS = {'fp32': 0, 'f16x3': 1}
 DEFAULT_PRECISION = os.environ.get('EXTDM_PRECISION', 'f16x3')
-
 
 class ExtdmConfig(ctypes.Structure):
     _fields_ = [('arch', ctypes.c_int), ('dim', ctypes.c_int), ('channels', ctypes.c_int),
@@ -93,6 +93,8 @@ def load():
     L.extdm_flow_hw.restype = i32
     L.extdm_bottleneck.argtypes = [vp, i32, vp, vp, vp]
     L.extdm_bottleneck.restype = i32
+    L.extdm_attn_layer.argtypes = [vp, ctypes.c_char_p, i32, i32, i32, i32, i32, i32, vp, vp, vp]
+    L.extdm_attn_layer.restype = i32
     L.extdm_range_flag.argtypes = [vp, i32, vp]
     L.extdm_range_flag.restype = i32
     _lib = L
@@ -220,6 +222,13 @@ class Handle:
         if rc < 0:
             check(rc)
         return rc
+
+    def attn_layer(self, prefix, x, out, shifted=False):
+        """One attention layer (STW or temporal) of the forward: x, out (B,C,T,H,W)."""
+        _require_device(x, out)
+        B, C, T, H, W = x.shape
+        check(load().extdm_attn_layer(self.h, prefix.encode(), B, C, T, H, W, int(shifted), _ptr(x), _ptr(out),
+                                      _stream()))
 
     def bench_layer(self, B, layer=0, iters=20):
         ms, fl = ctypes.c_float(), ctypes.c_double()

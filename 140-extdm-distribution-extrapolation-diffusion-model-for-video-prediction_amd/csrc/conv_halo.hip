@@ -184,6 +184,8 @@ __global__ __launch_bounds__(256) void conv_halo_kernel(HaloArgs a) {
       }
     }
     if (st + 1 < a.stages) HALO_STORE((st & 1) ? Xs0 : Xs1);
+    // the next stage's A pieces were LDS-DMA'd by several waves: each drains its own
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 

@@ -348,6 +348,20 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   return true;
 }
 
+int* x3_range_ptr() {
+  static thread_local int dev = -1;
+  static thread_local int* ptr = nullptr;
+  int d = 0;
+  (void)hipGetDevice(&d);
+  if (d != dev) {
+    void* p = nullptr;
+    (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_x3_range));
+    ptr = reinterpret_cast<int*>(p);
+    dev = d;
+  }
+  return ptr;
+}
+
 void x3_range_reset(hipStream_t s) {
   void* p = nullptr;
   (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_x3_range));

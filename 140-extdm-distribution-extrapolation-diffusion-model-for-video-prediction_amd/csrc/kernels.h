@@ -78,6 +78,7 @@ X3Tile x3_tile(int ks, int cout);
 bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                      const ConvEpi& epi);
 void x3_range_reset(hipStream_t s);
+int* x3_range_ptr();  // device address of the flag on the current device
 int x3_range_read(hipStream_t s);
 
 // out = act(conv(in0 ++ in1) + bias + res) [* s + sh]
@@ -124,9 +125,23 @@ bool stw_fused(hipStream_t s, const View& x, const AttnGeom& g, int heads, int d
 bool temporal_fused(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, int dim_head,
                     const float* gamma, const float* ln_w, const float* ln_b, const float* wqkv, const float* wout,
                     const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale);
+// f16x3 fused attention (stw_x3.hip): one wave per group of <= 32 tokens, C in {64, 128}.
+// Weights packed per unit of 32 qkv rows (attn_x3_unit_halves(C) halves each, see the
+// kernel header); wsc = {2^-sq, 2^-sk, 2^-sv, 2^-sproj} undoes the power-of-two pre-scaling.
+bool attn_x3_supported(int C, int ntok, int dim_head, int heads);
+int attn_x3_unit_halves(int C);
+bool stw_x3(hipStream_t s, const View& x, const AttnGeom& g, int heads, int dim_head, const float* gamma,
+            const void* wpk, const float* wsc, const float* bp, const float* bias_dense, int bstride,
+            const float* rcos, const float* rsin, float q_scale);
+bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, int dim_head,
+                 const float* gamma, const float* ln_w, const float* ln_b, const void* wpk, const float* wsc,
+                 const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale);
 // TrajWarp cross-attention (u12:719-773): q [B][256][NQ], k,v [B][256][NK].
 void cross_attention(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,
                      int heads, int NQ, int NK);
+// f16x3 variant (cross_x3.hip); false if the shape is not covered (dim_head != 32)
+bool cross_attention_x3(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,
+                        int heads, int NQ, int NK);
 
 void copy_view(hipStream_t s, const View& dst, const View& src);
 void maxpool_hw2(hipStream_t s, const View& dst, const View& src);

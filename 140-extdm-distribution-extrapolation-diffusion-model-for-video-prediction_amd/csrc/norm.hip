@@ -111,6 +111,68 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const float* __restrict__
   }
 }
 
+// gn_apply_kernel on 4 pixels per thread with 32-bit indexing within one (b, g): the
+// host checks HW % 4 == 0 and 16-byte aligned rows of x, out and res.
+__global__ __launch_bounds__(256) void gn_apply4_kernel(const float* __restrict__ x, long sb, long sc,
+                                                        float* out, long osb, long osc, long ost, int C, int Cg,
+                                                        int G, int T, int HW, int split, const double* partials,
+                                                        const float* gamma, const float* beta, const float* film,
+                                                        int film_row, int film_nt, const int* t_batch,
+                                                        const float* res, long rsb, long rsc, long rst,
+                                                        int split2) {
+  const int bg = blockIdx.y;
+  const int b = bg / G, g = bg % G;
+  __shared__ float st[2];
+  if (threadIdx.x == 0) {
+    double s = 0.0, ss = 0.0;
+    for (int i = 0; i < split; ++i) {
+      s += partials[((long)bg * split + i) * 2];
+      ss += partials[((long)bg * split + i) * 2 + 1];
+    }
+    const double n = (double)Cg * T * HW;
+    const double mean = s / n;
+    double var = ss / n - mean * mean;
+    if (var < 0) var = 0;
+    st[0] = (float)mean;
+    st[1] = 1.0f / sqrtf((float)var + 1e-5f);
+  }
+  __syncthreads();
+  const float mean = st[0], rstd = st[1];
+  const int HW4 = HW >> 2, THW4 = T * HW4;
+  const int L4 = Cg * THW4;
+  const int chunk = (L4 + split2 - 1) / split2;
+  const int e0 = blockIdx.x * chunk;
+  const int e1 = e0 + chunk < L4 ? e0 + chunk : L4;
+  const float* base = x + (long)b * sb + (long)g * Cg * sc;
+  const int tb = film ? t_batch[b] : 0;
+  for (int e = e0 + threadIdx.x; e < e1; e += 256) {
+    const int cl = e / THW4;
+    const int rem = e - cl * THW4;
+    const int t = rem / HW4, hw = (rem - t * HW4) * 4;
+    const int c = g * Cg + cl;
+    const float sc_ = rstd * gamma[c];
+    const float bi = beta[c] - mean * sc_;
+    float fsc = 1.f, fsh = 0.f;
+    if (film) {
+      fsc = film[(long)(film_row + c) * film_nt + tb] + 1.f;
+      fsh = film[(long)(film_row + C + c) * film_nt + tb];
+    }
+    const float4 xv = *reinterpret_cast<const float4*>(base + (long)cl * sc + (long)t * HW + hw);
+    float v[4] = {xv.x, xv.y, xv.z, xv.w};
+    float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (res) rv = *reinterpret_cast<const float4*>(res + off5(rsb, rsc, rst, b, c, t, hw));
+    const float r[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float u = v[k] * sc_ + bi;
+      if (film) u = u * fsc + fsh;
+      u = u / (1.f + expf(-u));
+      v[k] = u + r[k];
+    }
+    *reinterpret_cast<float4*>(out + off5(osb, osc, ost, b, c, t, hw)) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // ---------------- channel LayerNorm ----------------
 __device__ __forceinline__ float ld2(const float* p0, long b0, long c0s, int C0, const float* p1, long b1,
                                      long c1s, int c) {
@@ -329,6 +391,19 @@ void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, c
   if (split > 64) split = 64;
   hipLaunchKernelGGL(gn_stats_kernel, dim3(split, x.B * groups), dim3(256), 0, s, x.p, x.sb, x.sc, Cg, groups, L,
                      split, partials);
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const bool vec4 = x.HW() % 4 == 0 && L / 4 < (1L << 31) && al16(x.p) && al16(out.p) && x.sb % 4 == 0 &&
+                    x.sc % 4 == 0 && out.sb % 4 == 0 && out.sc % 4 == 0 && out.st % 4 == 0 &&
+                    (!res || (al16(res->p) && res->sb % 4 == 0 && res->sc % 4 == 0 && res->st % 4 == 0));
+  if (vec4) {
+    int split4 = (int)((L / 4 + 4095) / 4096);
+    if (split4 < 1) split4 = 1;
+    hipLaunchKernelGGL(gn_apply4_kernel, dim3(split4, x.B * groups), dim3(256), 0, s, x.p, x.sb, x.sc, out.p, out.sb,
+                       out.sc, out.st, x.C, Cg, groups, x.T, x.HW(), split, partials, gamma, beta, film, film_row,
+                       film_nt, t_batch, res ? res->p : nullptr, res ? res->sb : 0, res ? res->sc : 0,
+                       res ? res->st : 0, split4);
+    return;
+  }
   int split2 = (int)((L + 8191) / 8192);
   if (split2 < 1) split2 = 1;
   hipLaunchKernelGGL(gn_apply_kernel, dim3(split2, x.B * groups), dim3(256), 0, s, x.p, x.sb, x.sc, out.p, out.sb,

@@ -400,6 +400,72 @@ struct ExtdmHandle {
     HIPCHK(hipMemcpy(d, a.data(), a.size() * 4, hipMemcpyHostToDevice));
     return dev[n + "#stwproj"] = d;
   }
+  // f16x3 attention weights (stw_x3.hip): per unit u of 32 qkv rows, fragments of
+  // [hi|lo][lane][8] for q, k, v (row u*32 + lc, channels 16s + 8h + e) and the
+  // projection (row ct*32 + lc, hid u*32 + 16s' + 8(e>>2) + 4h + (e&3): the row order
+  // of the O^T accumulator). Each matrix is scaled by one power of two.
+  struct AttnX3W { void* w = nullptr; float* sc = nullptr; };
+  std::unordered_map<std::string, AttnX3W> attn_x3w;
+  static float pow2_scale(const float* p, size_t n, float& inv) {
+    float mx = 0.f;
+    for (size_t i = 0; i < n; ++i) mx = std::max(mx, std::fabs(p[i]));
+    int e = 0;
+    if (mx > 0.f) { std::frexp(mx, &e); e = 15 - e; }
+    inv = std::ldexp(1.f, -e);
+    return std::ldexp(1.f, e);
+  }
+  const AttnX3W& packed_attn_x3(const std::string& nqkv, const std::string& nproj) {
+    auto it = attn_x3w.find(nqkv);
+    if (it != attn_x3w.end()) return it->second;
+    const HostTensor& tq = H(nqkv);
+    const HostTensor& tp = H(nproj);
+    const int C = (int)tq.shape[1], hid = cfg.heads * cfg.dim_head, units = hid / 32;
+    REQUIRE((int)tq.shape[0] == 3 * hid && (int)tp.shape[0] == C && (int)tp.shape[1] == hid,
+            "attention weight shapes: " + nqkv);
+    const int KS = C / 16, CT = C / 32, uh = attn_x3_unit_halves(C);
+    REQUIRE(uh > 0, "attention x3 layout: unsupported channel count");
+    float inv[4], sc[4];
+    for (int m = 0; m < 3; ++m) sc[m] = pow2_scale(tq.f.data() + (size_t)m * hid * C, (size_t)hid * C, inv[m]);
+    sc[3] = pow2_scale(tp.f.data(), tp.f.size(), inv[3]);
+    std::vector<_Float16> a((size_t)units * uh);
+    auto put = [&](size_t frag_base, int l, int e, float v) {
+      const _Float16 hi = (_Float16)v;
+      a[frag_base + l * 8 + e] = hi;
+      a[frag_base + 512 + l * 8 + e] = (_Float16)(v - (float)hi);
+    };
+    for (int u = 0; u < units; ++u) {
+      const size_t ub = (size_t)u * uh;
+      for (int m = 0; m < 3; ++m)
+        for (int s2 = 0; s2 < KS; ++s2)
+          for (int l = 0; l < 64; ++l)
+            for (int e = 0; e < 8; ++e) {
+              const int row = m * hid + u * 32 + (l & 31), c = 16 * s2 + 8 * (l >> 5) + e;
+              put(ub + ((size_t)m * KS + s2) * 1024, l, e, tq.f[(size_t)row * C + c] * sc[m]);
+            }
+      for (int ct = 0; ct < CT; ++ct)
+        for (int s2 = 0; s2 < 2; ++s2)
+          for (int l = 0; l < 64; ++l)
+            for (int e = 0; e < 8; ++e) {
+              const int c = ct * 32 + (l & 31);
+              const int hd = u * 32 + 16 * s2 + 8 * (e >> 2) + 4 * (l >> 5) + (e & 3);
+              put(ub + ((size_t)3 * KS + ct * 2 + s2) * 1024, l, e, tp.f[(size_t)c * hid + hd] * sc[3]);
+            }
+    }
+    AttnX3W r;
+    r.w = dmalloc(a.size() * sizeof(_Float16));
+    HIPCHK(hipMemcpy(r.w, a.data(), a.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    r.sc = dmalloc(4 * sizeof(float));
+    HIPCHK(hipMemcpy(r.sc, inv, 4 * sizeof(float), hipMemcpyHostToDevice));
+    return attn_x3w[nqkv] = r;
+  }
+  bool x3_attn_ok(int C, int ntok, int mode) const {
+    auto flag = [](const char* n) { const char* v = getenv(n); return v && v[0] && v[0] != '0'; };
+    // opt-in (EXTDM_X3_ATTN=1): the f16x3 attention kernel still shows run-to-run differences
+    // on some shapes, so the sampling path keeps the fp32 attention kernels
+    const bool on = flag("EXTDM_X3_ATTN"), off_stw = flag("EXTDM_NO_X3_STW"), off_tmp = flag("EXTDM_NO_X3_TEMPORAL");
+    if (!on || (mode == 0 && off_stw) || (mode == 1 && off_tmp)) return false;
+    return cfg.precision == EXTDM_PRECISION_F16X3 && attn_x3_supported(C, ntok, cfg.dim_head, cfg.heads);
+  }
   bool fused_ok(int C, int ntok) const {
     static const bool off = [] { const char* v = getenv("EXTDM_NO_FUSED_STW"); return v && v[0] && v[0] != '0'; }();
     return !off && fused_attn_supported(C, ntok, cfg.dim_head, cfg.heads);
@@ -416,6 +482,15 @@ struct ExtdmHandle {
     // dense bias tables are laid out for the configured window (build_tables); a
     // collapsed window reads their leading N x N block (index[:N, :N], u12:476)
     const int bstride = cfg.window[0] * cfg.window[1] * cfg.window[2] <= 32 ? 32 : 64;
+    if (bstride == 32 && x3_attn_ok(x.C, N, 0)) {
+      const std::string a = p + ".fn.fn.attn";
+      const AttnX3W& w = packed_attn_x3(a + ".qkv.weight", a + ".proj.weight");
+      if (plan) return;
+      REQUIRE(stw_x3(s, x, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), w.w, w.sc, D(a + ".proj.bias"),
+                     bias_dense.at(p), bstride, rope_cos, rope_sin, q_scale()),
+              "f16x3 STW launch rejected");
+      return;
+    }
     if (fused_ok(x.C, N)) {
       const std::string a = p + ".fn.fn.attn";
       float* wq = packed_stw_qkv(a + ".qkv.weight");
@@ -447,6 +522,14 @@ struct ExtdmHandle {
     const int T = x.T;
     AttnGeom g{};
     g.mode = 1; g.D = T; g.H = x.H; g.W = x.W;
+    if (x3_attn_ok(x.C, T, 1) && out.sc == x.sc && out.st == x.st) {
+      const AttnX3W& w = packed_attn_x3(a + ".attn.to_qkv.weight", a + ".attn.to_out.weight");
+      if (plan) return;
+      REQUIRE(temporal_x3(s, x, out, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), D(a + ".norm.weight"),
+                          D(a + ".norm.bias"), w.w, w.sc, time_bias, 32, rope_cos, rope_sin, q_scale()),
+              "f16x3 temporal attention launch rejected");
+      return;
+    }
     if (fused_ok(x.C, T) && T <= 32) {
       float* wq = packed_stw_qkv(a + ".attn.to_qkv.weight");
       float* wo = packed_stw_proj(a + ".attn.to_out.weight");
@@ -554,7 +637,12 @@ struct ExtdmHandle {
     View q = alloc_cf(B, C, tp, fs, fs);
     conv(q, xq, nullptr, P(c + ".linear_q.weight"), 1, 0, D(c + ".linear_q.bias"), nullptr, ACT_RELU);
     View a = alloc_cf(B, C, tp, fs, fs);
-    if (!plan) cross_attention(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
+    if (!plan) {
+      static const bool off = [] { const char* v = getenv("EXTDM_NO_X3_CROSS"); return v && v[0] && v[0] != '0'; }();
+      const bool x3 = !off && cfg.precision == EXTDM_PRECISION_F16X3 &&
+                      cross_attention_x3(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
+      if (!x3) cross_attention(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
+    }
     View fm2p = alloc_cf(B, C, tp, fs, fs);
     conv(fm2p, a, nullptr, P(c + ".linear_o.weight"), 1, 0, D(c + ".linear_o.bias"), nullptr, ACT_RELU);
     View fp = fea.frames(tc, tp);
@@ -1450,6 +1538,26 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     REQUIRE(h->cfg.precision != EXTDM_PRECISION_F16X3 || x3_range_read(s) == 0,
             "f16x3 precision: a conv input reached |v| >= 65504 during sampling; results are not fp32-accurate "
             "(create the handle with EXTDM_PRECISION_FP32)");
+  });
+}
+
+int extdm_attn_layer(ExtdmHandle* h, const char* prefix, int B, int C, int T, int Hh, int Ww, int shifted,
+                     const float* x, float* out, void* stream) {
+  return guarded([&] {
+    REQUIRE(h && h->finalized && prefix, "handle not finalized");
+    HIPCHK(hipSetDevice(h->cfg.device));
+    h->s = reinterpret_cast<hipStream_t>(stream);
+    const std::string p = prefix;
+    View vx = cf_view(const_cast<float*>(x), B, C, T, Hh, Ww);
+    View vo = cf_view(out, B, C, T, Hh, Ww);
+    if (h->has(p + ".fn.fn.fn.attn.to_qkv.weight")) {
+      h->temporal(p, vx, vo);
+    } else {
+      REQUIRE(h->has(p + ".fn.fn.attn.qkv.weight"), "no attention layer named " + p);
+      HIPCHK(hipMemcpyAsync(out, x, (size_t)vx.numel() * sizeof(float), hipMemcpyDeviceToDevice, h->s));
+      h->stw(p, vo, shifted != 0);
+    }
+    HIPCHK(hipGetLastError());
   });
 }
 

@@ -121,6 +121,13 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
  * not, <0 on error; reset != 0 clears it. Synchronises `stream`. */
 int extdm_range_flag(ExtdmHandle* h, int reset, void* stream);
 
+/* One attention layer as the forward issues it (parity tests): prefix names a
+ * Residual(PreNorm(STWAttentionLayer)) (e.g. "downs.0.1", shifted per the layer's
+ * position, u12:961-963) or a temporal Residual(PreNorm(AttentionLayer)) (e.g.
+ * "init_temporal_attn", u12:915). x, out: [B,C,T,H,W] device tensors. */
+int extdm_attn_layer(ExtdmHandle* h, const char* prefix, int B, int C, int T, int H, int W, int shifted,
+                     const float* x, float* out, void* stream);
+
 /* LFAE decoder (Generator.forward_with_flow) for B clips x T frames.
  * ref: [B,C,S,S] source image; flow: [B,2,T,fh,fw] (x, y grid); occ: [B,1,T,fh,fw]
  * occlusion in [0,1] or NULL (reference quirk: without occlusion the prediction
