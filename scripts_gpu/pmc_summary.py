@@ -4,6 +4,7 @@ section): FETCH_SIZE counts half the bytes of 16-B/lane streaming reads -> x2.""
 import csv
 import glob
 import json
+import os
 import sys
 
 fetch_dir, write_dir, pattern, batch, out = sys.argv[1:6]
@@ -20,7 +21,7 @@ def rows(d, counter):
 
 fe = rows(fetch_dir, 'FETCH_SIZE')
 wr = rows(write_dir, 'WRITE_SIZE')
-res = {'kernel': pattern, 'batch': int(batch), 'launches': [len(fe), len(wr)],
+res = {'kernel': pattern, 'batch': int(batch), 'precision': os.environ.get('PREC', 'f16x3'), 'launches': [len(fe), len(wr)],
        'fetch_kb_raw_per_launch': sum(fe) / max(len(fe), 1), 'write_kb_per_launch': sum(wr) / max(len(wr), 1)}
 res['hbm_bytes_per_launch'] = int(2 * res['fetch_kb_raw_per_launch'] * 1024 + res['write_kb_per_launch'] * 1024)
 res['note'] = 'FETCH_SIZE doubled (gfx950 streaming-read correction); KB = 1024 B'
