@@ -460,10 +460,9 @@ struct ExtdmHandle {
   }
   bool x3_attn_ok(int C, int ntok, int mode) const {
     auto flag = [](const char* n) { const char* v = getenv(n); return v && v[0] && v[0] != '0'; };
-    // opt-in (EXTDM_X3_ATTN=1): the f16x3 attention kernel still shows run-to-run differences
-    // on some shapes, so the sampling path keeps the fp32 attention kernels
-    const bool on = flag("EXTDM_X3_ATTN"), off_stw = flag("EXTDM_NO_X3_STW"), off_tmp = flag("EXTDM_NO_X3_TEMPORAL");
-    if (!on || (mode == 0 && off_stw) || (mode == 1 && off_tmp)) return false;
+    // read per call: EXTDM_NO_X3_ATTN / _STW / _TEMPORAL route a layer back to the fp32 kernels
+    const bool off = flag("EXTDM_NO_X3_ATTN"), off_stw = flag("EXTDM_NO_X3_STW"), off_tmp = flag("EXTDM_NO_X3_TEMPORAL");
+    if (off || (mode == 0 && off_stw) || (mode == 1 && off_tmp)) return false;
     return cfg.precision == EXTDM_PRECISION_F16X3 && attn_x3_supported(C, ntok, cfg.dim_head, cfg.heads);
   }
   bool fused_ok(int C, int ntok) const {

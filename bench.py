@@ -177,7 +177,7 @@ def main():
             'metric': meta['metric'], 'value': round(value, 4), 'unit': 'frames/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(el / args.steps * 1e3, 2),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-            'dtype': 'fp32' if precision == 'fp32' else 'fp32 (f16x3 split-MFMA convs + TrajWarp attention, fp32 accumulate)',
+            'dtype': 'fp32' if precision == 'fp32' else 'fp32 (f16x3 split-MFMA convs + attention, fp32 accumulate)',
             'data': 'synthetic (U[0,1) PCG64 clips, seeded random-init weights; no dataset/checkpoint offline)',
             'config': {'workload': f'BAIR 64x64 ch3 {tc}->{args.total_pred} (tp={tp} x {rounds} rounds), '
                                    f'{sampler} steps, u12 Unet3D dim 64 mults (1,2,4,4), LFAE encoder + '
