@@ -237,6 +237,7 @@ void conv_forward(hipStream_t s, const View& out, const View& in0, const View* i
                   int stride, int pad, const ConvEpi& epi) {
   if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 && conv_x3_forward(s, out, in0, in1, w, epi))
     return;
+  if (conv_gemm_x3_forward(s, out, in0, in1, w, stride, pad, epi)) return;
   if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 && !getenv_flag("EXTDM_NO_HALO") &&
       conv_halo_forward(s, out, in0, in1, w, epi))
     return;

@@ -1,0 +1,304 @@
+// Implicit-GEMM convolution on fp16 MFMA with the f16x3 split (see conv_x3.hip): the
+// convs the direct kernel does not take -- strided Downsample (1,4,4)/s2 (u12:124-135),
+// the ConvTranspose parity GEMMs (u12:117-121), nearest-x2 up convs and small-Cin convs
+// such as init_noise_conv 3->256 7x7 (u12:914) and the LFAE convs (util.py:69-149).
+//   C[m][n] = sum_k A[m][k] B[k][n],  m = output channel, n = (b, t, oy, ox),
+//   k = (ci, ky, kx); B = im2col gathered on the fly from up to two channel sources.
+// Block tile BM x 128 x 32 (two MFMA k-steps), 256 threads = 4 waves, LDS double buffer
+// with a register prefetch of the next K tile (as conv.hip's fp32 kernel).
+// A is pre-packed per (mtile, ktile) as [step][m32][hi|lo][lane][8] (lane-linear 16-B
+// fragments, rows pre-scaled by powers of two, undone by gscale[m] in the epilogue);
+// B is split into hi / lo while staging, as [hi|lo][step][n][16 k] with the 16-B halves
+// of a row swapped on bit 3 of n (conflict-free ds_read_b128 over 16 lanes).
+#include <cstdlib>
+
+#include "kernels.h"
+
+namespace extdm {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+constexpr int BN = 128;
+constexpr int BK = 32;
+
+struct GArgs {
+  const float* in0; const float* in1;
+  long i0b, i0c, i0t, i1b, i1c, i1t;
+  int C0, Cin, Hin, Win;
+  const _Float16* w; const float* wscale; int nkt;
+  float* out; long ob, oc, ot;
+  int Cout, Ho, Wo, T, B;
+  int OWfull;
+  int stride, pad;
+  ConvEpi e;
+  long N;
+  int* range;
+};
+
+__device__ __forceinline__ float act_apply(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    case ACT_SILU: return v / (1.f + expf(-v));
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    default: return v;
+  }
+}
+
+template <int KH, int KW, int BM, int MODE>
+__global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
+  constexpr int WAVES_M = BM >= 64 ? 2 : 1;
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int TM = BM / (32 * WAVES_M);
+  constexpr int TN = BN / (32 * WAVES_N);
+  constexpr int KK = KH * KW;
+  constexpr int M32 = BM / 32;
+  constexpr int AH = 2 * M32 * 2 * 512;  // halves per A tile (2 steps, hi + lo)
+  constexpr int BH = 2 * 2 * BN * 16;    // halves per B tile ([hl][step][n][16])
+  constexpr int APASS = AH / 2048;       // 16-B chunks of 256 threads per A tile
+
+  extern __shared__ __attribute__((aligned(16))) _Float16 smg[];
+  _Float16* As0 = smg;
+  _Float16* As1 = smg + AH;
+  _Float16* Bs0 = smg + 2 * AH;
+  _Float16* Bs1 = Bs0 + BH;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WAVES_N;
+  const int wn = wave % WAVES_N;
+  const int h = lane >> 5, lc = lane & 31;
+  const long n0 = (long)blockIdx.x * BN;
+  const int mt = blockIdx.y;
+  const int par = blockIdx.z;  // deconv parity (py, px)
+  const int py = par >> 1, px = par & 1;
+  const _Float16* wbase = a.w + ((long)par * gridDim.y + mt) * a.nkt * AH;
+
+  // ---- per-thread gather column (B operand): column col, k groups kg and kg + 2 ----
+  const int col = tid & (BN - 1);
+  const int kg = tid >> 7;  // 0/1, uniform per wave
+  const long n = n0 + col;
+  const bool nvalid = n < a.N;
+  int iy0 = 0, ix0 = 0;
+  long base0 = 0, base1 = 0;
+  {
+    long nn = nvalid ? n : 0;
+    const int ox = (int)(nn % a.Wo); nn /= a.Wo;
+    const int oy = (int)(nn % a.Ho); nn /= a.Ho;
+    const int t = (int)(nn % a.T);
+    const int b = (int)(nn / a.T);
+    if (MODE == MODE_DECONV) {
+      iy0 = oy - (1 - py);
+      ix0 = ox - (1 - px);
+    } else {
+      iy0 = oy * a.stride - a.pad;
+      ix0 = ox * a.stride - a.pad;
+    }
+    base0 = (long)b * a.i0b + (long)t * a.i0t;
+    base1 = (long)b * a.i1b + (long)t * a.i1t;
+  }
+  const int Hv = MODE == MODE_UP2 ? 2 * a.Hin : a.Hin;
+  const int Wv = MODE == MODE_UP2 ? 2 * a.Win : a.Win;
+  const int K = a.Cin * KK;
+
+  float breg[2][8];
+  uint4 areg[APASS];
+  int bad = 0;
+
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int g2 = 0; g2 < 2; ++g2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int k = __builtin_amdgcn_readfirstlane(kt * BK + 8 * (kg + 2 * g2) + e);
+        const int ci = k / KK;
+        const int r = k - ci * KK;
+        const int ky = r / KW;
+        const int kx = r - ky * KW;
+        const int iy = iy0 + ky, ix = ix0 + kx;
+        float v = 0.f;
+        if (nvalid && k < K && iy >= 0 && iy < Hv && ix >= 0 && ix < Wv) {
+          const int sy = MODE == MODE_UP2 ? (iy >> 1) : iy;
+          const int sx = MODE == MODE_UP2 ? (ix >> 1) : ix;
+          const float* src = ci < a.C0 ? a.in0 + base0 + (long)ci * a.i0c
+                                       : a.in1 + base1 + (long)(ci - a.C0) * a.i1c;
+          v = src[(long)sy * a.Win + sx];
+        }
+        breg[g2][e] = v;
+      }
+    }
+    const uint4* ap = reinterpret_cast<const uint4*>(wbase + (long)kt * AH);
+#pragma unroll
+    for (int p = 0; p < APASS; ++p) areg[p] = ap[p * 256 + tid];
+  };
+  auto store_tile = [&](_Float16* As, _Float16* Bs) {
+#pragma unroll
+    for (int g2 = 0; g2 < 2; ++g2) {
+      const int g = kg + 2 * g2;  // 8-k group: step g >> 1, half g & 1
+      h8 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = breg[g2][e];
+        bad |= fabsf(v) >= 65504.f;
+        const _Float16 x = (_Float16)v;
+        hi[e] = x;
+        lo[e] = (_Float16)(v - (float)x);
+      }
+      _Float16* d = Bs + ((g >> 1) * BN + col) * 16 + 8 * ((g & 1) ^ ((col >> 3) & 1));
+      *reinterpret_cast<h8*>(d) = hi;
+      *reinterpret_cast<h8*>(d + 2 * BN * 16) = lo;
+    }
+    uint4* ad = reinterpret_cast<uint4*>(As);
+#pragma unroll
+    for (int p = 0; p < APASS; ++p) ad[p * 256 + tid] = areg[p];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  load_tile(0);
+  store_tile(As0, Bs0);
+  __syncthreads();
+  for (int kt = 0; kt < a.nkt; ++kt) {
+    const _Float16* As = (kt & 1) ? As1 : As0;
+    const _Float16* Bs = (kt & 1) ? Bs1 : Bs0;
+    if (kt + 1 < a.nkt) load_tile(kt + 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      h8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const _Float16* p = As + ((s * M32 + wm * TM + i) * 2) * 512 + lane * 8;
+        ah[i] = *reinterpret_cast<const h8*>(p);
+        al[i] = *reinterpret_cast<const h8*>(p + 512);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nc = (wn * TN + j) * 32 + lc;
+        const _Float16* p = Bs + (s * BN + nc) * 16 + 8 * (h ^ ((nc >> 3) & 1));
+        bh[j] = *reinterpret_cast<const h8*>(p);
+        bl[j] = *reinterpret_cast<const h8*>(p + 2 * BN * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (kt + 1 < a.nkt) store_tile((kt & 1) ? As0 : As1, (kt & 1) ? Bs0 : Bs1);
+    __syncthreads();
+  }
+  if (bad) atomicOr(a.range, 1);
+
+  // ---- epilogue (C/D map: col = lane & 31, row = (r&3) + 8(r>>2) + 4h) ----
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const long nn0 = n0 + (wn * TN + j) * 32 + lc;
+    if (nn0 >= a.N) continue;
+    long nn = nn0;
+    const int ox = (int)(nn % a.Wo); nn /= a.Wo;
+    const int oy = (int)(nn % a.Ho); nn /= a.Ho;
+    const int t = (int)(nn % a.T);
+    const int b = (int)(nn / a.T);
+    long pix;
+    if (MODE == MODE_DECONV) pix = (long)(2 * oy + py) * a.OWfull + (2 * ox + px);
+    else pix = (long)oy * a.Wo + ox;
+    const long obase = (long)b * a.ob + (long)t * a.ot + pix;
+    const long rbase = (long)b * a.e.res_sb + (long)t * a.e.res_st + pix;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mt * BM + (wm * TM + i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= a.Cout) continue;
+        float v = acc[i][j][r] * a.wscale[m];
+        if (a.e.bias) v += a.e.bias[m];
+        if (a.e.res) v += a.e.res[rbase + (long)m * a.e.res_sc];
+        if (a.e.post_scale) {
+          const long pi = a.e.post_per_channel ? (long)m : (long)b * a.Cout + m;
+          v = v * a.e.post_scale[pi] + a.e.post_shift[pi];
+        }
+        v = act_apply(v, a.e.act);
+        a.out[obase + (long)m * a.oc] = v;
+      }
+    }
+  }
+}
+
+template <int KH, int KW, int BM, int MODE>
+void launch(hipStream_t s, const GArgs& a, dim3 grid) {
+  constexpr int AH = 2 * (BM / 32) * 2 * 512, BH = 2 * 2 * BN * 16;
+  const size_t lds = (size_t)2 * (AH + BH) * sizeof(_Float16);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_x3_kernel<KH, KW, BM, MODE>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_gemm_x3_kernel<KH, KW, BM, MODE>), grid, dim3(256), lds, s, a);
+}
+
+template <int KH, int KW, int MODE>
+bool launch_bm(hipStream_t s, const GArgs& a, int bm, dim3 grid) {
+  if (bm == 128) launch<KH, KW, 128, MODE>(s, a, grid);
+  else if (bm == 64) launch<KH, KW, 64, MODE>(s, a, grid);
+  else if (bm == 32) launch<KH, KW, 32, MODE>(s, a, grid);
+  else return false;
+  return true;
+}
+
+}  // namespace
+
+int gemm_x3_bm(int M) { return conv_bm(M); }
+
+bool conv_gemm_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
+                          int stride, int pad, const ConvEpi& epi) {
+  if (!w.gx) return false;
+  GArgs a{};
+  a.in0 = in0.p; a.i0b = in0.sb; a.i0c = in0.sc; a.i0t = in0.st;
+  a.C0 = in0.C;
+  if (in1) { a.in1 = in1->p; a.i1b = in1->sb; a.i1c = in1->sc; a.i1t = in1->st; a.Cin = in0.C + in1->C; }
+  else { a.in1 = in0.p; a.i1b = in0.sb; a.i1c = in0.sc; a.i1t = in0.st; a.Cin = in0.C; }
+  a.Hin = in0.H; a.Win = in0.W;
+  a.w = reinterpret_cast<const _Float16*>(w.gx); a.wscale = w.gscale; a.nkt = w.gnkt;
+  a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st;
+  a.Cout = out.C; a.T = out.T; a.B = out.B;
+  a.stride = stride; a.pad = pad;
+  a.e = epi;
+  a.OWfull = out.W;
+  a.range = x3_range_ptr();
+  if (w.mode == MODE_DECONV) { a.Ho = in0.H; a.Wo = in0.W; }
+  else { a.Ho = out.H; a.Wo = out.W; }
+  a.N = (long)a.B * a.T * a.Ho * a.Wo;
+  if (a.Cin * w.KH * w.KW > a.nkt * BK || out.C > w.M) return false;
+  const int bm = w.gbm;
+  dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((w.M + bm - 1) / bm), w.mode == MODE_DECONV ? 4 : 1);
+  const int kh = w.KH, kw = w.KW, mode = w.mode;
+  if (mode == MODE_DECONV) {
+    if (kh == 2 && kw == 2) return launch_bm<2, 2, MODE_DECONV>(s, a, bm, grid);
+    return false;
+  }
+  if (mode == MODE_UP2) {
+    if (kh == 3 && kw == 3) return launch_bm<3, 3, MODE_UP2>(s, a, bm, grid);
+    return false;
+  }
+  if (kh == 1 && kw == 1) return launch_bm<1, 1, MODE_CONV>(s, a, bm, grid);
+  if (kh == 3 && kw == 3) return launch_bm<3, 3, MODE_CONV>(s, a, bm, grid);
+  if (kh == 4 && kw == 4) return launch_bm<4, 4, MODE_CONV>(s, a, bm, grid);
+  if (kh == 7 && kw == 7) return launch_bm<7, 7, MODE_CONV>(s, a, bm, grid);
+  return false;
+}
+
+}  // namespace extdm

@@ -50,6 +50,11 @@ struct PackedW {
   void* wx = nullptr;
   float* xscale = nullptr;
   int xbm = 0, xbn = 0, xng = 0, xncgb = 0;
+  // f16x3 implicit-GEMM layout [parity][mtile][ktile][step][m32][hi|lo][lane][8]
+  // (conv_gemm_x3.hip), rows pre-scaled by powers of two undone by gscale[m]
+  void* gx = nullptr;
+  float* gscale = nullptr;
+  int gbm = 0, gnkt = 0;
 };
 
 // Output-channel tile of the conv GEMM for M output channels (Mpad is a multiple of it).
@@ -137,6 +142,10 @@ bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& 
                  const float* gamma, const float* ln_w, const float* ln_b, const void* wpk, const float* wsc,
                  const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale);
 // TrajWarp cross-attention (u12:719-773): q [B][256][NQ], k,v [B][256][NK].
+// f16x3 implicit-GEMM conv (conv_gemm_x3.hip): every mode / kernel size of conv_forward's
+// fp32 GEMM; false if the weight has no f16x3 GEMM packing
+bool conv_gemm_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
+                          int stride, int pad, const ConvEpi& epi);
 void cross_attention(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,
                      int heads, int NQ, int NK);
 // f16x3 variant (cross_x3.hip); false if the shape is not covered (dim_head != 32)

@@ -159,7 +159,48 @@ struct ExtdmHandle {
     if (cfg.precision == EXTDM_PRECISION_F16X3 && kh == kw && (kh == 1 || kh == 3 || kh == 7) && co > 32 &&
         ci >= 16)
       pack_x3(pw, t.f, ci);
+    if (cfg.precision == EXTDM_PRECISION_F16X3) pack_gemm_x3(pw, a, 1);
     return packed[n] = pw;
+  }
+  // f16x3 implicit-GEMM layout (conv_gemm_x3.hip) from the fp32 GEMM packing a
+  // [npar][Kpad][Mpad]: [par][mtile][ktile][step][m32][hi|lo][lane][8], row m = mtile*BM +
+  // m32*32 + (lane & 31), k = ktile*32 + step*16 + 8*(lane >> 5) + e. Row m is scaled by
+  // 2^s(m) over all parities (max |w| -> [2^14, 2^15)), undone by gscale[m] = 2^-s(m).
+  void pack_gemm_x3(PackedW& pw, const std::vector<float>& a, int npar) {
+    const int M = pw.M, K = pw.K, bm = conv_bm(M);
+    const int nkt = (K + 31) / 32, mt = (M + bm - 1) / bm, m32 = bm / 32;
+    const size_t ah = (size_t)2 * m32 * 2 * 512, plane = (size_t)pw.Kpad * pw.Mpad;
+    std::vector<float> scale(M), rs(M);
+    for (int m = 0; m < M; ++m) {
+      float mx = 0.f;
+      for (int par = 0; par < npar; ++par)
+        for (int k = 0; k < K; ++k) mx = std::max(mx, std::fabs(a[par * plane + (size_t)k * pw.Mpad + m]));
+      int e = 0;
+      if (mx > 0.f) { std::frexp(mx, &e); e = 15 - e; }
+      scale[m] = std::ldexp(1.f, e);
+      rs[m] = std::ldexp(1.f, -e);
+    }
+    std::vector<_Float16> g((size_t)npar * mt * nkt * ah, (_Float16)0.f);
+    for (int par = 0; par < npar; ++par)
+      for (int mtile = 0; mtile < mt; ++mtile)
+        for (int kt = 0; kt < nkt; ++kt)
+          for (int st = 0; st < 2; ++st)
+            for (int q = 0; q < m32; ++q)
+              for (int l = 0; l < 64; ++l)
+                for (int e = 0; e < 8; ++e) {
+                  const int m = mtile * bm + q * 32 + (l & 31), k = kt * 32 + st * 16 + 8 * (l >> 5) + e;
+                  if (m >= M || k >= K) continue;
+                  const float v = a[par * plane + (size_t)k * pw.Mpad + m] * scale[m];
+                  const _Float16 hi = (_Float16)v;
+                  const size_t base = (((size_t)par * mt + mtile) * nkt + kt) * ah + (size_t)((st * m32 + q) * 2) * 512;
+                  g[base + l * 8 + e] = hi;
+                  g[base + 512 + l * 8 + e] = (_Float16)(v - (float)hi);
+                }
+    pw.gx = dmalloc(g.size() * sizeof(_Float16));
+    HIPCHK(hipMemcpy(pw.gx, g.data(), g.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    pw.gscale = dmalloc(M * sizeof(float));
+    HIPCHK(hipMemcpy(pw.gscale, rs.data(), M * sizeof(float), hipMemcpyHostToDevice));
+    pw.gbm = bm; pw.gnkt = nkt;
   }
   // f16x3 layout (conv_x3.hip): [mtile][cb*KS + ky][(g, kx)][m32][hi|lo][lane][8], lane =
   // (h, lc): row m = mtile*BM + m32*32 + lc, input channel cb*16NG + g*16 + 8h + e. Row m is
@@ -278,6 +319,7 @@ struct ExtdmHandle {
     }
     pw.w = dmalloc(a.size() * sizeof(float));
     HIPCHK(hipMemcpy(pw.w, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
+    if (cfg.precision == EXTDM_PRECISION_F16X3) pack_gemm_x3(pw, a, 4);
     return packed[n] = pw;
   }
   PackedW pack_matrix(const std::vector<float>& wrow /*[M][K]*/, int M, int K) {
