@@ -116,9 +116,10 @@ int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, fl
  * level-0 up ResnetBlock's 1x1 res_conv (ups.3.0.res_conv). */
 int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out, double* flops_out);
 
-/* The F16X3 activation-range flag: returns 1 if any conv input since the last
- * reset had |v| >= 65504 (results computed meanwhile are not fp32-accurate), 0 if
- * not, <0 on error; reset != 0 clears it. Synchronises `stream`. */
+/* The F16X3 activation-range flag: nonzero if an operand split since the last reset
+ * had |v| >= 65504 (results computed meanwhile are not fp32-accurate): bit 0 = a conv /
+ * GEMM / cross-attention input, bit 1 = a fused-attention operand; 0 if not, <0 on
+ * error; reset != 0 clears it. Synchronises `stream`. */
 int extdm_range_flag(ExtdmHandle* h, int reset, void* stream);
 
 /* One attention layer as the forward issues it (parity tests): prefix names a
