@@ -302,7 +302,12 @@ X3Tile x3_tile(int ks, int cout) {
   X3Tile t{};
   // 7x7 (init_conv): 16 waves over 64 x 512 px tiles, one X buffer; 3x3: 8 waves
   if (ks == 7) { t.bm = 64; t.bn = 512; t.ng = 1; }
-  else if (ks == 3) { if (cout <= 64) { t.bm = 64; t.bn = 256; } else { t.bm = 128; t.bn = 128; } t.ng = 1; }
+  else if (ks == 3) {
+    // EXTDM_X3_BN3: pixel tile of the Cout <= 64 3x3 convs (256 or 512)
+    static const int bn3 = [] { const char* v = getenv("EXTDM_X3_BN3"); return v ? atoi(v) : 256; }();
+    if (cout <= 64) { t.bm = 64; t.bn = bn3 == 512 ? 512 : 256; } else { t.bm = 128; t.bn = 128; }
+    t.ng = 1;
+  }
   else if (ks == 1) { t.bm = cout <= 64 ? 64 : 128; t.bn = 128; t.ng = 2; }
   return t;
 }

@@ -43,7 +43,7 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=1)
     ap.add_argument('--warmup', type=int, default=0)
-    ap.add_argument('--batch', type=int, default=32, help='clips per GPU')
+    ap.add_argument('--batch', type=int, default=64, help='clips per GPU')
     ap.add_argument('--sampling-steps', type=int, default=1000,
                     help='1000 = DDPM-1000 (the metric); fewer = DDIM-S (profiling sweeps only)')
     ap.add_argument('--total-pred', type=int, default=28)
