@@ -5,7 +5,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libextdm_hip.so')
+LIB_PATH = os.environ.get('EXTDM_LIB') or os.path.join(HERE, 'libextdm_hip.so')
 
 # every symbol include/extdm.h declares
 EXPORTS = ['extdm_create', 'extdm_destroy', 'extdm_last_error', 'extdm_load_weight', 'extdm_finalize',

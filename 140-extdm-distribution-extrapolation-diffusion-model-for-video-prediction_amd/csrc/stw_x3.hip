@@ -221,7 +221,18 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* __restric
   }
   // key-side token descriptors for the 16 keys j = dof(r, h) this lane's scores hold
   const bool shifted = MODE == 0 && (g.ss0 | g.ss1 | g.ss2) != 0;
-  const int desc = (me.lab & 0xFFFF) | (me.exists << 16) | (me.rpos << 17);
+  const int desc = (me.lab & 0xFFFF) | (me.exists << 16);
+  // The keys j = dof(r, h) of this lane's score registers do not depend on the unit:
+  // their masks are computed once (bit r), and their positions are known in closed
+  // form, so the bias loads carry no shuffle dependency and issue early.
+  unsigned kmis = 0, kgone = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int dj = __shfl(desc, dof(r, h));
+    kmis |= (unsigned)((dj & 0xFFFF) != me.lab) << r;
+    kgone |= (unsigned)(!((dj >> 16) & 1)) << r;
+  }
+  const int kper = g.D <= 16 ? 16 : 32;
 
   f32x16 pacc[CT];
 #pragma unroll
@@ -230,6 +241,14 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* __restric
     for (int r = 0; r < 16; ++r) pacc[i][r] = 0.f;
 
   const float sq = wsc[0] * q_scale, sk = wsc[1], sv = wsc[2];
+  // RoPE factors of this lane's (token, dim pair) registers: the same for every unit
+  float rc[8], rs[8];
+#pragma unroll
+  for (int r = 0; r < 16; r += 2) {
+    const int pi = (dof(r, h) % DH) >> 1;
+    rc[r >> 1] = rcos[me.rpos * RH + pi];
+    rs[r >> 1] = rsin[me.rpos * RH + pi];
+  }
   for (int u = 0; u < UNITS; ++u) {
     _Float16* W = wsm + (u & 1) * UL::HALVES;
     // unit u's slice has landed in every wave's pieces: LDS-DMA completion is tracked by
@@ -257,8 +276,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* __restric
     // scale, RoPE on (d, d+1) = registers (r, r+1); d = dof(r, h) within the head
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
-      const int pi = (dof(r, h) % DH) >> 1;
-      const float c = rcos[me.rpos * RH + pi], sn = rsin[me.rpos * RH + pi];
+      const float c = rc[r >> 1], sn = rs[r >> 1];
       const float q0 = q[r] * sq, q1 = q[r + 1] * sq;
       q[r] = q0 * c + (-q1) * sn;
       q[r + 1] = q1 * c + q0 * sn;
@@ -295,14 +313,14 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* __restric
       float mx = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int dj = __shfl(desc, dof(r, h));
-        float s_ = sc_[r] + bd[dj >> 17];
+        const int j = dof(r, h);
+        float s_ = sc_[r] + bd[MODE == 0 ? j : j % kper];
         if (MODE == 0) {
-          if (shifted && (dj & 0xFFFF) != me.lab) s_ += -100.f;
+          if (shifted && ((kmis >> r) & 1)) s_ += -100.f;
         } else {
-          if ((dj & 0xFFFF) != me.lab) s_ = -INFINITY;
+          if ((kmis >> r) & 1) s_ = -INFINITY;
         }
-        if (!((dj >> 16) & 1)) s_ = -INFINITY;
+        if ((kgone >> r) & 1) s_ = -INFINITY;
         sc_[r] = s_;
         mx = fmaxf(mx, s_);
       }
