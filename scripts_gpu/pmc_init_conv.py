@@ -11,6 +11,7 @@ import torch  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+layer = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # extdm_bench_layer id (0 = init_conv)
 pkg = importlib.import_module('140-extdm-distribution-extrapolation-diffusion-model-for-video-prediction_amd')
 torch.cuda.set_device(0)
 ucfg = pkg.spec.UnetConfig()
@@ -19,5 +20,5 @@ sd = pkg.weights.synth_state_dict(pkg.spec.unet_spec(ucfg), seed=1234)
 sd.update(pkg.schedule_buffers(1000))
 h.load_state(sd)
 h.finalize()
-ms, flops = h.bench_layer(B, 0, iters)
-print(f'init_conv B={B}: {ms:.3f} ms/launch, {flops / ms / 1e9:.1f} TFLOP/s')
+ms, flops = h.bench_layer(B, layer, iters)
+print(f'layer {layer} B={B}: {ms:.3f} ms/launch, {flops / ms / 1e9:.1f} TFLOP/s')
