@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void channel_ln_kernel(float* out, long osb, l
                                                          const float* p0, long sb0, long sc0, long st0, int C0,
                                                          const float* p1, long sb1, long sc1, long st1, int C,
                                                          int T, int HW, int B, const float* gamma) {
-  __shared__ double red[8][33];
+  __shared__ double red[8][33], red2[8][33];
   __shared__ float stat[2][32];
   const int px = threadIdx.x & 31, grp = threadIdx.x >> 5;
   const long idx = (long)blockIdx.x * 32 + px;
@@ -251,32 +251,26 @@ __global__ __launch_bounds__(256) void channel_ln_kernel(float* out, long osb, l
   const int b = (int)(id2 / ((long)HW * T));
   const long b0 = (long)b * sb0 + (long)t * st0 + hw;
   const long b1 = (long)b * sb1 + (long)t * st1 + hw;
-  double s = 0.0;
-  if (ok)
-    for (int c = grp; c < C; c += 8) s += ld2(p0, b0, sc0, C0, p1, b1, sc1, c);
-  red[grp][px] = s;
-  __syncthreads();
-  if (threadIdx.x < 32) {
-    double tt = 0.0;
-    for (int i = 0; i < 8; ++i) tt += red[i][threadIdx.x];
-    stat[0][threadIdx.x] = (float)(tt / C);
-    red[0][32] = 0.0;
-  }
-  __syncthreads();
-  const double mean = (double)stat[0][px];
-  double v2 = 0.0;
+  // one pass: sum and sum of squares in double (E[x^2] - mean^2 in double keeps the
+  // fp32 result of the two-pass form; a second read pass cost a quarter of the traffic)
+  double s = 0.0, ss = 0.0;
   if (ok)
     for (int c = grp; c < C; c += 8) {
-      const double d = ld2(p0, b0, sc0, C0, p1, b1, sc1, c) - mean;
-      v2 += d * d;
+      const double v = ld2(p0, b0, sc0, C0, p1, b1, sc1, c);
+      s += v;
+      ss += v * v;
     }
-  __syncthreads();
-  red[grp][px] = v2;
+  red[grp][px] = s;
+  red2[grp][px] = ss;
   __syncthreads();
   if (threadIdx.x < 32) {
-    double tt = 0.0;
-    for (int i = 0; i < 8; ++i) tt += red[i][threadIdx.x];
-    stat[1][threadIdx.x] = sqrtf((float)(tt / C) + 1e-5f);
+    double tt = 0.0, t2 = 0.0;
+    for (int i = 0; i < 8; ++i) { tt += red[i][threadIdx.x]; t2 += red2[i][threadIdx.x]; }
+    const double mean = tt / C;
+    double var = t2 / C - mean * mean;
+    if (var < 0) var = 0;
+    stat[0][threadIdx.x] = (float)mean;
+    stat[1][threadIdx.x] = sqrtf((float)var + 1e-5f);
   }
   __syncthreads();
   if (!ok) return;
