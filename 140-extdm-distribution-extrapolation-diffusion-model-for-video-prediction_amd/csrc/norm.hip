@@ -227,6 +227,73 @@ __global__ __launch_bounds__(256) void gn_apply4_kernel(const float* __restrict_
   }
 }
 
+// gn_apply4_kernel for large planes: one (b, c) channel per grid.y, so the channel's
+// scale / shift / FiLM are block constants and the element index needs no division
+// (frames contiguous in x, out and res: st == H*W). Same arithmetic per element.
+__global__ __launch_bounds__(256) void gn_apply_plane_kernel(const float* __restrict__ x, long sb, long sc,
+                                                             float* out, long osb, long osc, int C, int Cg, int G,
+                                                             int THW4, int split, const double* partials,
+                                                             const float* gamma, const float* beta,
+                                                             const float* film, int film_row, int film_nt,
+                                                             const int* t_batch, const float* res, long rsb,
+                                                             long rsc, int per) {
+  const int bc = blockIdx.y;
+  const int b = bc / C, c = bc - b * C;
+  const int bg = b * G + c / Cg;
+  __shared__ float st[2];
+  if (threadIdx.x == 0) {
+    double s = 0.0, ss = 0.0;
+    for (int i = 0; i < split; ++i) {
+      s += partials[((long)bg * split + i) * 2];
+      ss += partials[((long)bg * split + i) * 2 + 1];
+    }
+    const double n = (double)Cg * THW4 * 4;
+    const double mean = s / n;
+    double var = ss / n - mean * mean;
+    if (var < 0) var = 0;
+    st[0] = (float)mean;
+    st[1] = 1.0f / sqrtf((float)var + 1e-5f);
+  }
+  __syncthreads();
+  const float mean = st[0], rstd = st[1];
+  const float sc_ = rstd * gamma[c];
+  const float bi = beta[c] - mean * sc_;
+  float fsc = 1.f, fsh = 0.f;
+  if (film) {
+    const int tb = t_batch[b];
+    fsc = film[(long)(film_row + c) * film_nt + tb] + 1.f;
+    fsh = film[(long)(film_row + C + c) * film_nt + tb];
+  }
+  const float4* xp = reinterpret_cast<const float4*>(x + (long)b * sb + (long)c * sc);
+  float4* op = reinterpret_cast<float4*>(out + (long)b * osb + (long)c * osc);
+  const float4* rp = res ? reinterpret_cast<const float4*>(res + (long)b * rsb + (long)c * rsc) : nullptr;
+  const int i0 = blockIdx.x * per;
+  const int i1 = i0 + per < THW4 ? i0 + per : THW4;
+  for (int i = i0 + threadIdx.x; i < i1; i += 1024) {
+    float4 xv[4], rv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int iu = i + u * 256 < i1 ? i + u * 256 : i;
+      xv[u] = xp[iu];
+      rv[u] = rp ? rp[iu] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i + u * 256 >= i1) break;
+      float v[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+      const float r[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float w = v[k] * sc_ + bi;
+        if (film) w = w * fsc + fsh;
+        w = w / (1.f + expf(-w));
+        v[k] = w + r[k];
+      }
+      op[i + u * 256] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
 // ---------------- channel LayerNorm ----------------
 __device__ __forceinline__ float ld2(const float* p0, long b0, long c0s, int C0, const float* p1, long b1,
                                      long c1s, int c) {
@@ -488,6 +555,16 @@ void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, c
   const bool vec4 = x.HW() % 4 == 0 && L / 4 < (1L << 31) && al16(x.p) && al16(out.p) && x.sb % 4 == 0 &&
                     x.sc % 4 == 0 && out.sb % 4 == 0 && out.sc % 4 == 0 && out.st % 4 == 0 &&
                     (!res || (al16(res->p) && res->sb % 4 == 0 && res->sc % 4 == 0 && res->st % 4 == 0));
+  const int HW = x.HW();
+  if (vec4 && (long)x.T * HW / 4 >= 1024 && x.st == HW && out.st == HW && (!res || res->st == HW) &&
+      (long)x.B * x.C < 65536) {
+    const int THW4 = x.T * HW / 4;
+    const int per = 2048;  // float4 per block: eight per thread
+    hipLaunchKernelGGL(gn_apply_plane_kernel, dim3((THW4 + per - 1) / per, x.B * x.C), dim3(256), 0, s, x.p, x.sb,
+                       x.sc, out.p, out.sb, out.sc, x.C, Cg, groups, THW4, split, partials, gamma, beta, film,
+                       film_row, film_nt, t_batch, res ? res->p : nullptr, res ? res->sb : 0, res ? res->sc : 0, per);
+    return;
+  }
   if (vec4) {
     int split4 = (int)((L / 4 + 2047) / 2048);
     if (split4 < 1) split4 = 1;
