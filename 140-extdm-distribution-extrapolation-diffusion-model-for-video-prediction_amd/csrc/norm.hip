@@ -496,15 +496,30 @@ __global__ __launch_bounds__(256) void adaptor_stats_kernel(const float* x, long
   const float* p = x + (long)b * sb + (long)c * sc;
   const int n = T * HW;
   double s = 0.0, dummy = 0.0;
-  for (int e = threadIdx.x; e < n; e += 256) s += p[(long)(e / HW) * st + e % HW];
+  // (t, hw) of element e tracked incrementally (no division per element); same order
+  const int t0 = threadIdx.x / HW, hw0 = threadIdx.x - t0 * HW;
+  const int dt = 256 / HW, dhw = 256 - dt * HW;
+  {
+    int t = t0, hw = hw0;
+    for (int e = threadIdx.x; e < n; e += 256) {
+      s += p[(long)t * st + hw];
+      t += dt; hw += dhw;
+      if (hw >= HW) { hw -= HW; ++t; }
+    }
+  }
   __shared__ double sh[8];
   block_sum2(s, dummy, sh);
   const double mean = s / n;
   double v2 = 0.0;
   dummy = 0.0;
-  for (int e = threadIdx.x; e < n; e += 256) {
-    const double d = p[(long)(e / HW) * st + e % HW] - mean;
-    v2 += d * d;
+  {
+    int t = t0, hw = hw0;
+    for (int e = threadIdx.x; e < n; e += 256) {
+      const double d = p[(long)t * st + hw] - mean;
+      v2 += d * d;
+      t += dt; hw += dhw;
+      if (hw >= HW) { hw -= HW; ++t; }
+    }
   }
   __syncthreads();
   block_sum2(v2, dummy, sh);
@@ -514,17 +529,16 @@ __global__ __launch_bounds__(256) void adaptor_stats_kernel(const float* x, long
   }
 }
 
+// one (b, c) per grid.y, 32-bit (t, hw) within it (the flat 64-bit div/mod chain dominated)
 __global__ __launch_bounds__(256) void adaptor_norm_kernel(float* d, long dsb, long dsc, long dst_, const float* s,
                                                            long ssb, long ssc, long sst, int C, int T, int HW,
-                                                           const float* mean, const float* std_, long total) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= total) return;
-  const int hw = (int)(idx % HW);
-  long r = idx / HW;
-  const int t = (int)(r % T); r /= T;
-  const int c = (int)(r % C);
-  const int b = (int)(r / C);
-  d[off5(dsb, dsc, dst_, b, c, t, hw)] = (s[off5(ssb, ssc, sst, b, c, t, hw)] - mean[b * C + c]) / std_[b * C + c];
+                                                           const float* mean, const float* std_) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= T * HW) return;
+  const int bc = blockIdx.y;
+  const int b = bc / C, c = bc - b * C;
+  const int t = e / HW, hw = e - t * HW;
+  d[off5(dsb, dsc, dst_, b, c, t, hw)] = (s[off5(ssb, ssc, sst, b, c, t, hw)] - mean[bc]) / std_[bc];
 }
 
 inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
@@ -627,9 +641,13 @@ void adaptor_stats(hipStream_t s, const View& x, float* mean, float* std_, doubl
 }
 
 void adaptor_normalize(hipStream_t s, const View& d, const View& src, const float* mean, const float* std_) {
-  const long total = d.numel();
-  hipLaunchKernelGGL(adaptor_norm_kernel, dim3(nblk(total)), dim3(256), 0, s, d.p, d.sb, d.sc, d.st, src.p, src.sb,
-                     src.sc, src.st, d.C, d.T, d.HW(), mean, std_, total);
+  const int bstep = 65535 / d.C;  // grid.y limit
+  for (int b0 = 0; b0 < d.B; b0 += bstep) {
+    const int nb = d.B - b0 < bstep ? d.B - b0 : bstep;
+    hipLaunchKernelGGL(adaptor_norm_kernel, dim3(nblk((long)d.T * d.HW()), nb * d.C), dim3(256), 0, s,
+                       d.p + (long)b0 * d.sb, d.sb, d.sc, d.st, src.p + (long)b0 * src.sb, src.sb, src.sc, src.st,
+                       d.C, d.T, d.HW(), mean + (long)b0 * d.C, std_ + (long)b0 * d.C);
+  }
 }
 
 }  // namespace extdm
