@@ -488,6 +488,56 @@ __global__ __launch_bounds__(256) void bilinear4_kernel(float* d, long dsb, long
   }
 }
 
+// Small input planes (Hi*Wi <= 1024): BPLS (b, c) planes of one frame per block are
+// staged into LDS with coalesced loads, the 2-D interpolation gathers from LDS and each
+// thread stores float4 runs. Same lin_idx weights and expression as bilinear_kernel.
+constexpr int BPLS = 8;
+__global__ __launch_bounds__(256) void bilinear_lds_kernel(float* d, long dsb, long dsc, long dst_, const float* a,
+                                                           long asb, long asc, long ast, const float* bb, long bsb,
+                                                           long bsc, long bst, int tsplit, int C, int nbc, int Ho,
+                                                           int Wo, int Hi, int Wi, int vec) {
+  __shared__ float pl[BPLS * 1024];
+  const int t = blockIdx.y;
+  const int bc0 = blockIdx.x * BPLS;
+  const int np = nbc - bc0 < BPLS ? nbc - bc0 : BPLS;
+  const int HWi = Hi * Wi;
+  for (int k = threadIdx.x; k < np * HWi; k += 256) {
+    const int j = k / HWi, e = k - j * HWi;
+    const int bc = bc0 + j;
+    const int b = bc / C, c = bc - b * C;
+    const float* p = t < tsplit ? a + off5(asb, asc, ast, b, c, t, 0) : bb + off5(bsb, bsc, bst, b, c, t - tsplit, 0);
+    pl[j * HWi + e] = p[e];
+  }
+  __syncthreads();
+  const int n4 = Ho * Wo / 4;
+  for (int k = threadIdx.x; k < np * n4; k += 256) {
+    const int j = k / n4, q = k - j * n4;
+    const int bc = bc0 + j;
+    const int b = bc / C, c = bc - b * C;
+    const int y = 4 * q / Wo, x = 4 * q - y * Wo;
+    int y0, y1;
+    float ly0, ly1;
+    lin_idx(y, Hi, Ho, y0, y1, ly0, ly1);
+    const float* r0 = pl + j * HWi + y0 * Wi;
+    const float* r1 = pl + j * HWi + y1 * Wi;
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int x0, x1;
+      float lx0, lx1;
+      lin_idx(x + u, Wi, Wo, x0, x1, lx0, lx1);
+      v[u] = ly0 * (lx0 * r0[x0] + lx1 * r0[x1]) + ly1 * (lx0 * r1[x0] + lx1 * r1[x1]);
+    }
+    float* o = d + off5(dsb, dsc, dst_, b, c, t, y * Wo + x);
+    if (vec) {
+      *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) o[u] = v[u];
+    }
+  }
+}
+
 // ---------------- MotionAdaptor ----------------
 __global__ __launch_bounds__(256) void adaptor_stats_kernel(const float* x, long sb, long sc, long st, int C, int T,
                                                             int HW, float* mean_out, float* std_out) {
@@ -624,6 +674,14 @@ void maxpool_hw2(hipStream_t s, const View& d, const View& src) {
 
 void bilinear_frames(hipStream_t s, const View& d, const View& a, const View& b, int t_split) {
   const long total = d.numel();
+  if (d.W % 4 == 0 && a.H * a.W <= 1024 && d.T < 65536 && a.H == b.H && a.W == b.W) {
+    const int vec = ((uintptr_t)d.p & 15) == 0 && d.sb % 4 == 0 && d.sc % 4 == 0 && d.st % 4 == 0;
+    const int nbc = d.B * d.C;
+    hipLaunchKernelGGL(bilinear_lds_kernel, dim3((nbc + BPLS - 1) / BPLS, d.T), dim3(256), 0, s, d.p, d.sb, d.sc,
+                       d.st, a.p, a.sb, a.sc, a.st, b.p, b.sb, b.sc, b.st, t_split, d.C, nbc, d.H, d.W, a.H, a.W,
+                       vec);
+    return;
+  }
   if (d.W % 4 == 0 && (long)d.B * d.C < 65536 && d.T < 65536) {
     const int vec = ((uintptr_t)d.p & 15) == 0 && d.sb % 4 == 0 && d.sc % 4 == 0 && d.st % 4 == 0;
     const int n4 = d.H * d.W / 4;
