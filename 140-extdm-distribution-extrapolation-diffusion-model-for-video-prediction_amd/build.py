@@ -1,5 +1,9 @@
 """Build libextdm_hip.so (gfx950) in-tree with hipcc: the .so travels with the
-repository snapshot to the GPU box. No torch extension machinery is involved."""
+repository snapshot to the GPU box. No torch extension machinery is involved.
+
+`build(variant=..., opt=..., extra=...)` builds an A/B copy of the library into
+_variants/<variant>/ (per-file optimisation levels / extra flags) for the GPU
+measurement scripts (EXTDM_LIB selects it at run time)."""
 import os
 import subprocess
 import sys
@@ -10,14 +14,16 @@ CSRC = os.path.join(HERE, 'csrc')
 REPO = os.path.dirname(HERE)
 INCLUDE = os.path.join(REPO, 'include')
 LIB = os.path.join(HERE, 'libextdm_hip.so')
-SOURCES = ['conv.hip', 'conv_halo.hip', 'conv_x3.hip', 'conv_gemm_x3.hip', 'norm.hip', 'attn.hip', 'stw_fused.hip', 'stw_x3.hip', 'cross_x3.hip', 'sampler.hip', 'decoder.hip', 'lfae.hip', 'runtime.cpp']
+SOURCES = ['conv.hip', 'conv_halo.hip', 'conv_x3.hip', 'conv_gemm_x3.hip', 'norm.hip', 'attn.hip', 'stw_fused.hip',
+           'stw_x3.hip', 'cross_x3.hip', 'sampler.hip', 'decoder.hip', 'lfae.hip', 'runtime.cpp']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-I', INCLUDE, '-I', CSRC]
-# Per-file optimisation level. The fused f16x3 attention kernels feed MFMA results straight
-# back into VALU / MFMA operands; built at -O3 (ROCm 7.2) they give run-to-run differences
-# on gfx950 (suspected missing MFMA->VALU wait states in the -O3 schedule), at -O1 they are
-# bit-stable and agree with the oracle (scripts_gpu/attn_diag.py, tests/test_gpu_attn.py).
-OPT = {'stw_x3.hip': '-O1', 'cross_x3.hip': '-O1'}
+# Per-file flags. The fused f16x3 attention kernels (many independent fp32 lanes of
+# work between MFMAs) must not be SLP-vectorised: at -O3 the SLP pass turns their
+# scalar fp32 arithmetic into v_pk_mul_f32 / v_pk_add_f32 pairs (DESIGN.md §4.0 build
+# note), which also pushes the 8-wave C = 64 kernels past 256 VGPRs into scratch.
+PER_FILE = {'stw_x3.hip': ['-fno-slp-vectorize'], 'cross_x3.hip': ['-fno-slp-vectorize']}
+OPT = {}
 
 
 def _needs(obj, src):
@@ -27,26 +33,34 @@ def _needs(obj, src):
     return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 
-def _compile(src):
-    obj = os.path.join(CSRC, 'build', src + '.o')
+def _compile(src, objdir, opt, per_file, extra):
+    obj = os.path.join(objdir, src + '.o')
     s = os.path.join(CSRC, src)
     if _needs(obj, s):
-        flags = [OPT.get(src, f) if f == '-O3' else f for f in FLAGS]
+        flags = [opt.get(src, f) if f == '-O3' else f for f in FLAGS] + per_file.get(src, []) + extra.get(src, [])
         cmd = [HIPCC] + flags + (['-x', 'hip'] if src.endswith('.cpp') else []) + ['-c', s, '-o', obj]
         subprocess.run(cmd, check=True)
     return obj
 
 
-def build(verbose=False):
-    os.makedirs(os.path.join(CSRC, 'build'), exist_ok=True)
+def build(verbose=False, variant=None, opt=None, per_file=None, extra=None):
+    if variant:
+        objdir = os.path.join(REPO, '_variants', variant, 'obj')
+        lib = os.path.join(REPO, '_variants', variant, 'libextdm_hip.so')
+    else:
+        objdir, lib = os.path.join(CSRC, 'build'), LIB
+    opt = OPT if opt is None else opt
+    per_file = PER_FILE if per_file is None else per_file
+    extra = extra or {}
+    os.makedirs(objdir, exist_ok=True)
     jobs = int(os.environ.get('MAX_JOBS', '8'))
     with ThreadPoolExecutor(max_workers=min(jobs, len(SOURCES))) as ex:
-        objs = list(ex.map(_compile, SOURCES))
-    if not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        subprocess.run([HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', LIB] + objs, check=True)
+        objs = list(ex.map(lambda s: _compile(s, objdir, opt, per_file, extra), SOURCES))
+    if not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in objs):
+        subprocess.run([HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', lib] + objs, check=True)
     if verbose:
-        print('built', LIB)
-    return LIB
+        print('built', lib)
+    return lib
 
 
 if __name__ == '__main__':

@@ -39,6 +39,9 @@ _DATASETS = {
             ('VideoFlowDiffusion_multi_w_ref_u22', 'DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_ada_u22')),
 }
 
+# valid_params.type (kth.yaml names its split 'valid')
+_VALID_TYPE = {'kth': 'valid'}
+
 WRAPPERS = {'VideoFlowDiffusion_multi_w_ref': 'multi_w_ref', 'VideoFlowDiffusion_multi_w_ref_u22': 'multi_w_ref_u22',
             'VideoFlowDiffusion_multi1248': 'multi1248'}
 
@@ -60,12 +63,25 @@ def dm_config(name, pred_frames=None, sampling_timesteps=10, estimate_occlusion_
         'dataset_params': {'frame_shape': S,
                            'train_params': {'type': 'train', 'cond_frames': tc,
                                             'pred_frames': tp if pred_frames is None else pred_frames},
-                           'valid_params': {'type': 'test', 'cond_frames': vc, 'pred_frames': vp}},
+                           'valid_params': {'type': _VALID_TYPE.get(name, 'test'), 'cond_frames': vc,
+                                            'pred_frames': vp}},
         'flow_params': {'model_params': fp},
         'diffusion_params': {'model_params': {'null_cond_prob': 0.0, 'use_residual_flow': False,
                                               'only_use_flow': False, 'sampling_timesteps': sampling_timesteps,
                                               'loss_type': 'l2', 'ada_layers': 'auto'}},
     }
+
+
+def load_dm_config(path, estimate_occlusion_map=None):
+    """A config/DM YAML file as valid.py loads it (yaml.safe_load), with the
+    `--estimate_occlusion_map` CLI override applied (valid.py:78-81) when given."""
+    import yaml
+    with open(path) as f:
+        cfg = yaml.safe_load(f)
+    if estimate_occlusion_map is not None:
+        pf = cfg['flow_params']['model_params']['generator_params']['pixelwise_flow_predictor_params']
+        pf['estimate_occlusion_map'] = bool(estimate_occlusion_map)
+    return cfg
 
 
 def dm_arch(name):

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
       h8 hi, lo;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float v = breg[g2][e];
+        const float v = split_src(breg[g2][e]);
         bad |= fabsf(v) >= 65504.f;
         const _Float16 x = (_Float16)v;
         hi[e] = x;

@@ -157,7 +157,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
       h8 hi0, hi1, lo0, lo1;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const float v0 = xr[j][c], v1 = xr[j][c + 8];
+        const float v0 = split_src(xr[j][c]), v1 = split_src(xr[j][c + 8]);
         range_bad |= (fabsf(v0) >= 65504.f) | (fabsf(v1) >= 65504.f);
         const _Float16 a0 = (_Float16)v0, a1 = (_Float16)v1;
         hi0[c] = a0; hi1[c] = a1;

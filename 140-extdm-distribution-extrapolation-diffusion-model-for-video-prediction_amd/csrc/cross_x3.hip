@@ -33,7 +33,7 @@ constexpr float LO_UP = 2048.f, LO_DN = 1.f / 2048.f;
 // hi = fp16(v), lo = fp16((v - hi) * 2^11), into vector elements
 #define SPLIT_S(V, HI, LO)                              \
   do {                                                  \
-    const float v_ = (V);                               \
+    const float v_ = split_src(V);                      \
     const _Float16 a_ = (_Float16)v_;                   \
     HI = a_;                                            \
     LO = (_Float16)((v_ - (float)a_) * LO_UP);          \

@@ -11,6 +11,15 @@
 
 namespace extdm {
 
+// f16x3 operand split: hi = fp16(v), lo = fp16(v - hi) from ONE opaque fp32 value.
+// Without the barrier hipcc (ROCm 7.2, gfx950) may lower the two uses of fp16(v) of a
+// product v differently (v_cvt_pk_f16_f32 of the rounded product for hi, v_fma_mixlo_f16
+// of the exact product inside lo), and hi + lo then misses v by an fp16 ulp.
+__device__ __forceinline__ float split_src(float v) {
+  asm("" : "+v"(v));
+  return v;
+}
+
 struct View {
   float* p = nullptr;
   int B = 0, C = 0, T = 0, H = 0, W = 0;

@@ -7,6 +7,7 @@
 // Reductions accumulate in double so the fp32 outputs track the reference's
 // fp32 reductions to rounding.
 #include "kernels.h"
+#include <stdexcept>
 
 namespace extdm {
 
@@ -598,6 +599,10 @@ inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, const float* gamma,
                     const float* beta, const float* film, int film_row, int film_nt, const int* t_batch,
                     const View* res, double* partials) {
+  // the statistics kernels read each (b, group) as Cg*T*H*W contiguous floats
+  if (x.st != x.HW() || x.sc != (long)x.T * x.HW() || x.C % groups != 0)
+    throw std::invalid_argument("groupnorm_silu: input must be [B][C][T][H][W] with contiguous (C, T, H, W) "
+                                "per sample and C divisible by the group count");
   const int Cg = x.C / groups;
   const long L = (long)Cg * x.T * x.HW();
   int split = (int)((L + 32767) / 32768);

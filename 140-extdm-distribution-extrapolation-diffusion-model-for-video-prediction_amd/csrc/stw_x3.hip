@@ -80,13 +80,18 @@ __device__ __forceinline__ Tok token_of(int tk, const AttnGeom& g, long st, int 
   return o;
 }
 
+// hi = fp16(v), lo = fp16(v - hi) of an opaque v (split_src, kernels.h): the
+// probabilities and scaled q / k / v here are products, whose two fp16 roundings hipcc
+// would otherwise lower differently (hi + lo off by an fp16 ulp in ~2^-13 of the values;
+// it made the reciprocal-multiply softmax fail at 2.7e-4).
 __device__ __forceinline__ void split8(const float* v, h8& hi, h8& lo, int& bad) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    bad |= fabsf(v[e]) >= 65504.f;
-    const _Float16 a = (_Float16)v[e];
+    const float w = split_src(v[e]);
+    bad |= fabsf(w) >= 65504.f;
+    const _Float16 a = (_Float16)w;
     hi[e] = a;
-    lo[e] = (_Float16)(v[e] - (float)a);
+    lo[e] = (_Float16)(w - (float)a);
   }
 }
 
@@ -108,7 +113,8 @@ struct UnitLayout {
 };
 
 template <int C, int MODE, int DH, int NW>
-__global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* __restrict__ x, float* __restrict__ out,
+// x and out alias for the in-place STW layers (MODE 0): no __restrict__ on them.
+__global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float* out,
                                                           long sb, long sc, long st, long osb, long osc, AttnGeom g,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ ln_w,
@@ -329,8 +335,9 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* __restric
 #pragma unroll
       for (int r = 0; r < 16; ++r) { sc_[r] = expf(sc_[r] - mx); sum += sc_[r]; }
       sum += __shfl_xor(sum, 32);
+      const float inv = 1.f / sum;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sc_[r] = sc_[r] / sum;
+      for (int r = 0; r < 16; ++r) sc_[r] *= inv;
       // O^T[dd][i] = sum_j V^T[dd][j] P^T[j][i]; lanes of the unit's other head masked
       const bool mine = HPU == 1 || (lc / DH) == hh;
 #pragma unroll

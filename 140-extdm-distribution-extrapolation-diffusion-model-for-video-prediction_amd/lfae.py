@@ -238,6 +238,10 @@ class FlowDiffusion(nn.Module):
         if wrapper == 'multi1248' and not self.estimate_occlusion_map:
             # multi1248.py:236 reads generated["occlusion_map"] unconditionally
             raise KeyError('occlusion_map: the multi1248 wrapper needs estimate_occlusion_map=True')
+        if wrapper == 'multi_w_ref_u22' and not self.estimate_occlusion_map:
+            # multi_w_ref_u22.py:496-498 decodes with occlusion_map=sample_conf.to(...): None has no .to
+            raise AttributeError("'NoneType' object has no attribute 'to': the multi_w_ref_u22 wrapper needs "
+                                 "estimate_occlusion_map=True")
         S = ds['frame_shape']
         self.generator = Generator(num_regions=fp['num_regions'], num_channels=fp['num_channels'],
                                    revert_axis_swap=fp['revert_axis_swap'], image_size=S, **fp['generator_params'])
@@ -349,14 +353,15 @@ class FlowDiffusion(nn.Module):
 
 @torch.no_grad()
 def autoregressive_sample(model, real_vids, total_pred_frames, num_sample_video=1, cond_scale=1.0, seed=None,
-                          sample_base=0):
+                          sample_base=0, round_noise=None):
     """The eval driver's generation loop (scripts/DM/valid.py:141-186): clips
     repeated n times as '(b n)', NUM_AUTOREG = ceil(total / tp) rounds of
     sample_one_video, each conditioned on the last tc decoded frames of the
     previous round. Returns cat(real cond frames, predictions)[:, :, :tc + total].
     With `seed`, round r draws its noise from the counter-based stream keyed by
     (seed, global sample index = sample_base + i, round r), so shards of a batch
-    reproduce the unsharded run."""
+    reproduce the unsharded run. `round_noise[r]` = (x_T, noise) injects round r's
+    noise instead (parity tests replaying the reference's CPU stream)."""
     from math import ceil
     tc, tp = model.cond_frame_num, model.pred_frame_num
     vids = real_vids.repeat_interleave(num_sample_video, dim=0)
@@ -364,6 +369,8 @@ def autoregressive_sample(model, real_vids, total_pred_frames, num_sample_video=
     preds = []
     for r in range(ceil(total_pred_frames / tp)):
         kw = {} if seed is None else {'seed': seed, 'sample_base': sample_base, 'round_idx': r}
+        if round_noise is not None:
+            kw = {'x_T': round_noise[r][0], 'noise': round_noise[r][1]}
         out = model.sample_one_video(cond_scale=cond_scale, real_vid=cur, **kw)['sample_out_vid']
         preds.append(out[:, :, -tp:])
         cur = out[:, :, -tc:].contiguous()

@@ -14,6 +14,7 @@ state_dict key layout follow the reference, so reference checkpoints load with
 `Unet3D.forward` run unmodified. Compute always goes through libextdm_hip.so
 on a ROCm device; a CPU tensor is an error, not a fallback.
 """
+import dataclasses
 import math
 
 import torch
@@ -94,8 +95,24 @@ class Unet3D(nn.Module):
     def _state_version(self):
         return tuple((p.data_ptr(), p._version) for p in self.parameters())
 
+    def set_fea_size(self, n):
+        """cond_fea's spatial size. The reference resizes cond_fea to the latent inside
+        forward whatever its size (ada / ada_u22: F.interpolate, ada_u22.py:1230-1234), so
+        the same module serves e.g. Cityscapes' 32x32 bottleneck (multi_w_ref_u22 passes
+        it unresized) and BAIR-style 16x16 ones; the native handle is sized per fea_size.
+        u12's TrajWarp needs the maxpooled latent (latent / 2), wo_ref the latent itself."""
+        n = int(n)
+        if n == self.ucfg.fea_size:
+            return
+        if self.ARCH in (ARCH_U12, ARCH_U22) and n != self.ucfg.latent // 2:
+            raise AssertionError(f'u12 TrajWarp needs cond_fea at latent / 2 = {self.ucfg.latent // 2}, got {n}')
+        if self.ARCH == ARCH_WO_REF and n != self.ucfg.latent:
+            raise AssertionError(f'wo_ref concatenates cond_fea at the latent size {self.ucfg.latent}, got {n}')
+        self.ucfg = dataclasses.replace(self.ucfg, fea_size=n)
+
     def native(self, timesteps_buffers, max_batch, device_index):
-        ver = (self._state_version(), id(timesteps_buffers), max_batch, device_index, self.precision)
+        ver = (self._state_version(), id(timesteps_buffers), max_batch, device_index, self.precision,
+               self.ucfg.fea_size)
         if self._native is None or self._native_version != ver:
             h = _lib.Handle(self.ucfg, int(timesteps_buffers['betas'].shape[0]), max_batch, device_index,
                             precision=self.precision)
@@ -130,6 +147,7 @@ class Unet3D(nn.Module):
         assert cond_fea.shape[2] == self.ucfg.frames
         if not x.is_cuda:
             raise RuntimeError('ExtDM HIP path needs tensors on a ROCm device (no CPU fallback)')
+        self.set_fea_size(cond_fea.shape[-1])
         B = x.shape[0]
         h = self.native(self._sched(), max(B, getattr(self, 'max_batch', 1)), x.device.index or 0)
         out = torch.empty_like(x)
@@ -224,7 +242,9 @@ class GaussianDiffusion(nn.Module):
         self.max_batch = 1
         self.use_graph = True
 
-    def _native(self, B, device):
+    def _native(self, B, device, fea_size=None):
+        if fea_size is not None:
+            self.denoise_fn.set_fea_size(fea_size)
         bufs = {k: getattr(self, k).detach().to('cpu') for k in schedule_buffers(1).keys()}
         self._bufs_cache = getattr(self, '_bufs_cache', None)
         if self._bufs_cache is None or any(not torch.equal(self._bufs_cache[k], bufs[k]) for k in bufs):
@@ -249,7 +269,7 @@ class GaussianDiffusion(nn.Module):
         out = x.clone().contiguous()
         tt = int(t[0].item())
         assert bool((t == tt).all()), 'the native step takes one t for the whole batch'
-        h = self._native(x.shape[0], x.device)
+        h = self._native(x.shape[0], x.device, cond_fea.shape[-1])
         h.sampler_step(_lib.SAMPLER_DDPM, tt, 0, 0., out, eps.contiguous(), noise.contiguous()[None])
         return out
 
@@ -264,7 +284,7 @@ class GaussianDiffusion(nn.Module):
         B = shape[0]
         out = torch.empty(shape, device=device, dtype=torch.float32)
         times = list(reversed(range(self.num_timesteps)))
-        h = self._native(B, device)
+        h = self._native(B, device, cond_fea.shape[-1])
         h.sample(_lib.SAMPLER_DDPM, times, None, 0., x_cond.float().contiguous(), cond_fea.float().contiguous(), out,
                  x_T=x_T, noise=noise, seed=self._seed() if seed is None else seed, sample_base=sample_base,
                  round_idx=round_idx, use_graph=self.use_graph)
@@ -279,7 +299,7 @@ class GaussianDiffusion(nn.Module):
         B = shape[0]
         pairs = ddim_time_pairs(self.num_timesteps, self.sampling_timesteps)
         out = torch.empty(shape, device=device, dtype=torch.float32)
-        h = self._native(B, device)
+        h = self._native(B, device, cond_fea.shape[-1])
         h.sample(_lib.SAMPLER_DDIM, [p[0] for p in pairs], [p[1] for p in pairs], self.ddim_sampling_eta,
                  x_cond.float().contiguous(), cond_fea.float().contiguous(), out, x_T=x_T, noise=noise,
                  seed=self._seed() if seed is None else seed, sample_base=sample_base, round_idx=round_idx,

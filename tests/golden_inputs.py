@@ -41,6 +41,42 @@ LFAE_CFG = _spec.LfaeConfig()
 FD_UNET = _spec.UnetConfig(tc=2, tp=4)
 
 
+_configs = importlib.import_module(PKG + '.configs')
+# sample_one_video of the other two FlowDiffusion wrappers (tests/golden/wrappers.npz), DDIM-10:
+#   u22    VideoFlowDiffusion_multi_w_ref_u22.py:415-510, Cityscapes 128 px (20 regions, perspective
+#          background, scale 0.25: flow 32x32, cond_fea = the 32x32 bottleneck), ada_u22 denoiser
+#   m1248  VideoFlowDiffusion_multi1248.py:213-295, SMMNIST 10 -> 5, wo_ref denoiser (dims 1-2-4-8),
+#          cond_fea bilinear to the flow size, occlusion on (App. A.2)
+WRAP_CASES = {
+    'u22': {'module': 'VideoFlowDiffusion_multi_w_ref_u22', 'wrapper': 'multi_w_ref_u22',
+            'config': lambda: _configs.dm_config('cityscapes', sampling_timesteps=10),
+            'unet': _for(_spec.ARCH_ADA_U22, tc=2, tp=5, latent=32, fea_size=32), 'B': 1, 'seed': 12,
+            'noise_seed': 41},
+    'm1248': {'module': 'VideoFlowDiffusion_multi1248', 'wrapper': 'multi1248',
+              'config': lambda: _configs.dm_config('smmnist', sampling_timesteps=10),
+              'unet': _for(_spec.ARCH_WO_REF, tc=10, tp=5, latent=32), 'B': 1, 'seed': 13, 'noise_seed': 43},
+}
+# the eval driver's autoregressive loop (valid.py:150-171): 1 clip x n=2 samples, 2 rounds of
+# tp = 4 -> 7 delivered frames, BAIR eval default (no occlusion map)
+AR_CASE = {'unet': FD_UNET, 'occ': False, 'B': 1, 'n': 2, 'total': 7, 'seed': 14, 'noise_seed': 45}
+
+
+def ddpm100_case():
+    """DDPM on the timesteps=100 schedule with the wo_ref denoiser (SMMNIST BASELINE config)."""
+    cfg = CONFIGS['woref_small']
+    x, _, cond, fea = unet_inputs(cfg, B=2, seed=23)
+    return cfg, x, cond, fea, 47
+
+
+def ddim_noise(shape, S=10):
+    """The CPU noise stream one reference ddim_sample consumes after torch.manual_seed:
+    x_T, then a draw for every step whose time_next > 0 (Diffusion.py:217, 250); the
+    last step draws nothing (zeros injected)."""
+    xT = torch.randn(shape)
+    noise = [torch.randn(shape) for _ in range(S - 1)] + [torch.zeros(shape)]
+    return xT, torch.stack(noise)
+
+
 def make_sd(cfg, seed=1234):
     return _w.synth_state_dict(_spec.unet_spec(cfg), seed=seed, window=cfg.window)
 

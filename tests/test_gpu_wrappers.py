@@ -1,0 +1,117 @@
+"""GPU parity of the paths VERDICT r1 found unpinned, against outputs of the
+reference itself (tests/golden/wrappers.npz, tests/golden/make_golden.py wrappers()):
+
+  * sample_one_video of VideoFlowDiffusion_multi_w_ref_u22 (:415-510; Cityscapes
+    128 px, 20 regions, perspective background, ada_u22 denoiser, cond_fea = the
+    32x32 bottleneck) and of VideoFlowDiffusion_multi1248 (:213-295; SMMNIST 10 -> 5,
+    wo_ref denoiser, occlusion on), DDIM-10;
+  * two rounds of the eval driver's autoregressive loop (scripts/DM/valid.py:150-171)
+    with the multi_w_ref wrapper, '(b n)' repeat, decoded frames fed back;
+  * a DDPM chain over the timesteps=100 schedule (SMMNIST BASELINE config).
+
+The reference's CPU noise stream is replayed and injected. Tolerances: a whole
+sample_one_video round 1e-3 abs (as tests/test_gpu_lfae.py); two chained rounds
+2e-3 (round 2 re-encodes round 1's decoded frames); DDPM-100 chain 5e-4.
+"""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_inputs import (AR_CASE, LFAE_CFG, PKG, WRAP_CASES, ddim_noise, ddpm100_case, lfae_config_dict,
+                                 make_lfae_sd, make_sd, video_inputs)
+from tests.test_oracle_golden import load
+
+pytestmark = pytest.mark.gpu
+
+pkg = importlib.import_module(PKG)
+spec = importlib.import_module(PKG + '.spec')
+DEV = torch.device('cuda:0')
+
+
+def _wrapper_model(case):
+    cfgd = case['config']()
+    lc = spec.LfaeConfig.from_config(cfgd)
+    fd = pkg.FlowDiffusion(config=cfgd, is_train=False, wrapper=case['wrapper'],
+                           dim_mults=case['unet'].dim_mults, Unet3D_architecture=case['unet'].arch).to(DEV)
+    sds = make_lfae_sd(lc)
+    fd.generator.load_state_dict(sds['generator'])
+    fd.region_predictor.load_state_dict(sds['region_predictor'])
+    fd.bg_predictor.load_state_dict(sds['bg_predictor'])
+    fd.unet.load_state_dict(make_sd(case['unet']))
+    return fd, lc
+
+
+@pytest.mark.parametrize('tag', sorted(WRAP_CASES))
+def test_wrapper_sample_one_video_vs_reference(tag):
+    case = WRAP_CASES[tag]
+    g = load('wrappers.npz')
+    fd, lc = _wrapper_model(case)
+    u = case['unet']
+    vid = video_inputs(B=case['B'], T=u.tc, S=lc.image, seed=case['seed'])
+    torch.manual_seed(case['noise_seed'])
+    xT, noise = ddim_noise((case['B'], 3, u.tp, u.latent, u.latent))
+    ret = fd.sample_one_video(1.0, vid.to(DEV), x_T=xT.to(DEV), noise=noise.to(DEV).contiguous())
+    keys = sorted(k[len(tag) + 1:] for k in g.files if k.startswith(tag + '_'))
+    assert sorted(ret) == keys
+    for k in keys:
+        err = np.abs(ret[k].cpu().numpy() - g[f'{tag}_{k}']).max()
+        assert err <= 1e-3, (k, err)
+
+
+def test_u22_wrapper_needs_occlusion_like_the_reference():
+    case = WRAP_CASES['u22']
+    cfgd = case['config']()
+    cfgd['flow_params']['model_params']['generator_params']['pixelwise_flow_predictor_params'][
+        'estimate_occlusion_map'] = False
+    with pytest.raises(AttributeError):
+        pkg.FlowDiffusion(config=cfgd, is_train=False, wrapper='multi_w_ref_u22')
+
+
+def test_autoregressive_two_rounds_vs_reference():
+    import dataclasses
+    c = AR_CASE
+    u = c['unet']
+    lc = dataclasses.replace(LFAE_CFG, pf_estimate_occlusion_map=c['occ'])
+    fd = pkg.FlowDiffusion(config=lfae_config_dict(lc, u, c['occ']), is_train=False, dim_mults=u.dim_mults,
+                           Unet3D_architecture='DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_u12').to(DEV)
+    sds = make_lfae_sd(lc)
+    fd.generator.load_state_dict(sds['generator'])
+    fd.region_predictor.load_state_dict(sds['region_predictor'])
+    fd.bg_predictor.load_state_dict(sds['bg_predictor'])
+    fd.unet.load_state_dict(make_sd(u))
+    real = video_inputs(B=c['B'], T=u.tc, seed=c['seed'])
+    rounds = -(-c['total'] // u.tp)
+    torch.manual_seed(c['noise_seed'])
+    shape = (c['B'] * c['n'], 3, u.tp, u.latent, u.latent)
+    rn = []
+    for _ in range(rounds):
+        xT, noise = ddim_noise(shape)
+        rn.append((xT.to(DEV), noise.to(DEV).contiguous()))
+    out = pkg.autoregressive_sample(fd, real.to(DEV), c['total'], num_sample_video=c['n'], round_noise=rn)
+    g = load('wrappers.npz')['ar_result']
+    assert out.shape == g.shape
+    err = np.abs(out.cpu().numpy() - g).max()
+    assert err <= 2e-3, err
+
+
+def test_ddpm100_chain_vs_reference():
+    cfg, x, cond, fea, seed = ddpm100_case()
+    g = load('wrappers.npz')
+    sch = pkg.schedule_buffers(100)
+    assert np.array_equal(sch['betas'].numpy(), g['sched100_betas'])
+    h = pkg._lib.Handle(cfg, 100, x.shape[0], 0)
+    sd = make_sd(cfg)
+    sd.update(sch)
+    h.load_state(sd)
+    h.finalize()
+    torch.manual_seed(seed)
+    xT = torch.randn(x.shape)
+    noises = torch.stack([torch.randn(x.shape) for _ in range(100)])  # p_sample draws at every t, t = 0 included
+    out = torch.empty(x.shape, device=DEV)
+    h.sample(0, list(range(99, -1, -1)), None, 0., cond.to(DEV), fea.to(DEV), out, x_T=xT.to(DEV),
+             noise=noises.to(DEV).contiguous(), use_graph=True)
+    torch.cuda.synchronize()
+    err = np.abs(out.cpu().numpy() - g['ddpm100']).max()
+    assert err <= 5e-4, err
