@@ -153,6 +153,18 @@ bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& 
 // TrajWarp cross-attention (u12:719-773): q [B][256][NQ], k,v [B][256][NK].
 // f16x3 implicit-GEMM conv (conv_gemm_x3.hip): every mode / kernel size of conv_forward's
 // fp32 GEMM; false if the weight has no f16x3 GEMM packing
+// init_conv's x-branch composed with init_noise_conv into 49 border-class 13x13
+// kernels (xpath_x3.hip): out[:, :Cout] = sum_c K_c * x + cbias_c for the 3-channel x
+struct XPathArgs {
+  const float* x; long xb, xc, xt;
+  int T, L, F;
+  float* out; long ob, oc, ot; int Cout;
+  const _Float16* w; const float* rscale; const float* cbias;
+  int* range;
+  int tile_start[50];
+};
+bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
+                      const float* cbias);
 bool conv_gemm_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                           int stride, int pad, const ConvEpi& epi);
 void cross_attention(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,

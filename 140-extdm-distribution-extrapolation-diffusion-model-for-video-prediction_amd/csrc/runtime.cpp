@@ -336,6 +336,104 @@ struct ExtdmHandle {
     return pw;
   }
 
+  // init_conv's x-branch composed with init_noise_conv (xpath_x3.hip): 49 border-class
+  // 13x13 kernels over the 3 latent channels, built in fp64, packed as f16x3 A fragments
+  // [class][kstep = (ci, dy)][m32][hi|lo][lane][8] (row m = m32*32 + (lane & 31), column
+  // dx = 8*(lane >> 5) + e, zero for dx >= 13), rows scaled by 2^s(class, m).
+  struct XPathW { void* w = nullptr; float* rs = nullptr; float* cb = nullptr; };
+  XPathW xpw;
+  bool xpath_ready = false;
+  bool xpath_enabled() const {
+    static const bool off = [] { const char* v = getenv("EXTDM_NO_XPATH"); return v && v[0] && v[0] != '0'; }();
+    return !off && cfg.precision == EXTDM_PRECISION_F16X3 &&
+           (cfg.arch == EXTDM_ARCH_U12 || cfg.arch == EXTDM_ARCH_ADA) && cfg.latent >= 7 && cfg.dim <= 64;
+  }
+  const XPathW& Pxpath() {
+    if (xpath_ready) return xpw;
+    const HostTensor& wn = H("init_noise_conv.weight");  // [Cm][3][1][7][7]
+    const HostTensor& bnt = H("init_noise_conv.bias");
+    const HostTensor& wi = H("init_conv.weight");        // [Co][Cm + Cf][1][7][7]
+    const HostTensor& bit = H("init_conv.bias");
+    const int Cm = (int)wn.shape[0], Ci = (int)wn.shape[1], Co = (int)wi.shape[0], Cin = (int)wi.shape[1];
+    REQUIRE(Ci == 3 && wn.shape.back() == 7 && wi.shape.back() == 7 && Cin > Cm && Co <= 64,
+            "composed init_conv: unexpected init_noise_conv / init_conv shapes");
+    const int L = cfg.latent, M32 = (Co + 31) / 32, MP = M32 * 32;
+    // V[m][ci][a][b][e][f] = sum_c' Wa[m][c'][a][b] Wn[c'][ci][e][f]; U[m][a][b] = sum_c' Wa bn
+    std::vector<double> V((size_t)Co * 3 * 49 * 49, 0.0), U((size_t)Co * 49, 0.0);
+    for (int m = 0; m < Co; ++m)
+      for (int ab = 0; ab < 49; ++ab)
+        for (int c = 0; c < Cm; ++c) {
+          const double wa = wi.f[((size_t)m * Cin + c) * 49 + ab];
+          if (wa == 0.0) continue;
+          U[(size_t)m * 49 + ab] += wa * bnt.f[c];
+          for (int ci = 0; ci < 3; ++ci) {
+            const float* pn = &wn.f[((size_t)c * 3 + ci) * 49];
+            double* pv = &V[(((size_t)m * 3 + ci) * 49 + ab) * 49];
+            for (int ef = 0; ef < 49; ++ef) pv[ef] += wa * pn[ef];
+          }
+        }
+    // tap a of a class (offset a - 3 from p) is valid iff p + a - 3 lies in [0, L)
+    auto valid = [&](int cls1, int a) {
+      const int p = cls1 < 3 ? cls1 : (cls1 == 3 ? 3 : L - 7 + cls1);
+      const int q = p + a - 3;
+      return cls1 == 3 || (q >= 0 && q < L);
+    };
+    const size_t per_cls = (size_t)3 * 13 * M32 * 1024;
+    std::vector<_Float16> g(49 * per_cls, (_Float16)0.f);
+    std::vector<float> rs((size_t)49 * MP, 0.f), cb((size_t)49 * MP, 0.f);
+    std::vector<double> K((size_t)Co * 3 * 169);
+    for (int cls = 0; cls < 49; ++cls) {
+      const int cy = cls / 7, cx = cls % 7;
+      std::fill(K.begin(), K.end(), 0.0);
+      for (int m = 0; m < Co; ++m) {
+        double cbv = bit.f[m];
+        for (int a = 0; a < 7; ++a)
+          for (int b = 0; b < 7; ++b) {
+            if (!valid(cy, a) || !valid(cx, b)) continue;
+            cbv += U[(size_t)m * 49 + a * 7 + b];
+            for (int ci = 0; ci < 3; ++ci) {
+              const double* pv = &V[(((size_t)m * 3 + ci) * 49 + a * 7 + b) * 49];
+              double* pk = &K[((size_t)m * 3 + ci) * 169];
+              for (int e = 0; e < 7; ++e)
+                for (int f = 0; f < 7; ++f) pk[(a + e) * 13 + (b + f)] += pv[e * 7 + f];
+            }
+          }
+        cb[(size_t)cls * MP + m] = (float)cbv;
+        double mx = 0.0;
+        for (int k = 0; k < 3 * 169; ++k) mx = std::max(mx, std::fabs(K[(size_t)m * 3 * 169 + k]));
+        int e2 = 0;
+        if (mx > 0.0) { std::frexp(mx, &e2); e2 = 15 - e2; }
+        rs[(size_t)cls * MP + m] = std::ldexp(1.f, -e2);
+        for (int ci = 0; ci < 3; ++ci)
+          for (int dy = 0; dy < 13; ++dy)
+            for (int dx = 0; dx < 13; ++dx) {
+              const float v = (float)std::ldexp(K[((size_t)m * 3 + ci) * 169 + dy * 13 + dx], e2);
+              const int ks = ci * 13 + dy, m32 = m / 32, lane = (m % 32) + 32 * (dx / 8), e = dx % 8;
+              const size_t base = (size_t)cls * per_cls + ((size_t)ks * M32 + m32) * 1024;
+              const _Float16 hi = (_Float16)v;
+              g[base + lane * 8 + e] = hi;
+              g[base + 512 + lane * 8 + e] = (_Float16)(v - (float)hi);
+            }
+      }
+    }
+    xpw.w = dmalloc(g.size() * sizeof(_Float16));
+    HIPCHK(hipMemcpy(xpw.w, g.data(), g.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    xpw.rs = dmalloc(rs.size() * sizeof(float));
+    HIPCHK(hipMemcpy(xpw.rs, rs.data(), rs.size() * sizeof(float), hipMemcpyHostToDevice));
+    xpw.cb = dmalloc(cb.size() * sizeof(float));
+    HIPCHK(hipMemcpy(xpw.cb, cb.data(), cb.size() * sizeof(float), hipMemcpyHostToDevice));
+    // the fea branch alone: init_conv.weight[:, Cm:]
+    HostTensor fw;
+    fw.shape = {Co, (int64_t)(Cin - Cm), 1, 7, 7};
+    fw.f.resize((size_t)Co * (Cin - Cm) * 49);
+    for (int m = 0; m < Co; ++m)
+      std::copy(wi.f.begin() + ((size_t)m * Cin + Cm) * 49, wi.f.begin() + ((size_t)m * Cin + Cin) * 49,
+                fw.f.begin() + (size_t)m * (Cin - Cm) * 49);
+    host["init_conv.weight#fea"] = std::move(fw);
+    xpath_ready = true;
+    return xpw;
+  }
+
   View alloc_cf(int B, int C, int T, int Hh, int Ww) {
     return cf_view(arena.alloc((size_t)B * C * T * Hh * Ww), B, C, T, Hh, Ww);
   }
@@ -778,8 +876,14 @@ struct ExtdmHandle {
         View fu = with_batch(fup_all, B).frames(tc, tp);
         conv(rp, vx, &fu, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
       } else {
-        View x0p = alloc_cf(B, 256, tp, L, L);
-        conv(x0p, vx, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
+        // x0p = init_noise_conv(x) is only materialised where TrajWarp reads it (u12); with
+        // the composed x-branch init_conv needs just x itself
+        const bool xp = xpath_enabled();
+        View x0p;
+        if (arch == EXTDM_ARCH_U12 || !xp) {
+          x0p = alloc_cf(B, 256, tp, L, L);
+          conv(x0p, vx, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
+        }
         View fu;
         if (arch == EXTDM_ARCH_U12) {
           View fp2 = alloc_cf(B, cfg.fea_ch, tp, fs, fs);
@@ -789,7 +893,14 @@ struct ExtdmHandle {
         } else {
           fu = with_batch(fup_all, B).frames(tc, tp);
         }
-        conv(rp, x0p, &fu, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+        if (xp) {
+          // rp = K_class * x + cbias_class (x-branch + both biases), then rp += Wb * pad(fu)
+          const XPathW& xw = Pxpath();
+          if (!plan) REQUIRE(xpath_x3_forward(s, rp, vx, xw.w, xw.rs, xw.cb), "composed init_conv launch rejected");
+          conv(rp, fu, nullptr, P("init_conv.weight#fea"), 1, 3, nullptr, &rp);
+        } else {
+          conv(rp, x0p, &fu, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+        }
       }
     }
     View xt = alloc_cf(B, d0, T, L, L);
@@ -1631,12 +1742,19 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
                                   "downs.2.0.block2.proj.weight", "ups.3.0.res_conv.weight"};
     static const int levels[] = {0, 0, 1, 2, 0};
     REQUIRE(layer >= 0 && layer < 5, "unknown layer id");
-    const std::string wn = names[layer];
+    std::string wn = names[layer];
+    // with the composed x-branch (xpath_x3.hip) the forward's init_conv launch is the
+    // cond_fea branch alone: 256 -> 64 channels (init_conv.weight[:, 256:])
+    const bool fea_only = layer == 0 && h->xpath_enabled();
+    if (fea_only) {
+      h->Pxpath();
+      wn = "init_conv.weight#fea";
+    }
     REQUIRE(h->has(wn), "bench layer weight missing: " + wn);
     const auto& sh = h->H(wn).shape;
     const int co = (int)sh[0], ci = (int)sh[1], ks = (int)sh.back();
     const int Lq = L >> levels[layer];
-    const int c1 = layer == 0 ? h->cfg.fea_ch : 0, c0 = ci - c1;
+    const int c1 = layer == 0 && !fea_only ? h->cfg.fea_ch : 0, c0 = ci - c1;
     View x0 = h->alloc_cf(B, c0, T, Lq, Lq);
     View fup = c1 ? h->alloc_cf(B, c1, T, Lq, Lq) : x0;
     View r = h->alloc_cf(B, co, T, Lq, Lq);

@@ -1,0 +1,165 @@
+// init_conv's x-branch folded with init_noise_conv (u12:913-914, 1029-1041; ada the
+// same), f16x3 MFMA.
+//
+// The reference computes
+//     r = init_conv(cat(init_noise_conv(x), fu))              (1,7,7) convs, pad 3
+// i.e. r = Wa * pad(x0) + Wb * pad(fu) + b with x0 = Wn * pad(x) + bn (3 -> 256 ch)
+// and Wa the first 256 input channels of init_conv. Both branches are linear, so
+// Wa * pad(x0) is ONE 13x13 convolution of the 3-channel x with the composed
+// kernel Wa o Wn, except that pad(x0) is zero outside the latent: the intermediate
+// positions q = p + (a-3, b-3) that fall outside [0, L) drop out. Which ones do
+// depends only on how close p is to each border, so there are 7 classes per axis
+// (0, 1, 2, interior, L-3, L-2, L-1) and 49 composed kernels
+//     K_c[m][ci][dy][dx] = sum_{(a,b) valid for c} sum_c' Wa[m][c'][a][b] Wn[c'][ci][dy-a][dx-b]
+// plus the per-class constant sum_{(a,b) valid} sum_c' Wa[m][c'][a][b] bn[c'] + b[m]
+// (built in fp64 at extdm_finalize, runtime.cpp pack_xpath). That is 3*169 MACs per
+// output channel instead of 256*49 (the x-branch was half of init_conv's FLOPs).
+//
+// The kernel is an implicit GEMM per class: M = Cout (32 * M32), K = 3 ch x 13 rows x
+// 16 columns (13 used), N = the class's pixels over all frames (a class's pixel set
+// is rows(cy) x cols(cx) of every frame). One wave owns 64 pixels (two n32 tiles) and
+// all output channels; A (the class's packed weights, [kstep][m32][hl][lane][8]) is
+// read straight from L2, B is gathered from x (8 consecutive columns per lane and
+// k-step) and split into hi / lo in registers. No LDS, no barriers.
+#include "kernels.h"
+
+namespace extdm {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+constexpr int KSTEPS = 3 * 13;  // (ci, dy); 16 dx columns per step
+
+__device__ __forceinline__ f32x16 mma3(const h8& ah, const h8& al, const h8& bh, const h8& bl, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
+  return c;
+}
+
+__device__ __forceinline__ void class_span(int c, int L, int& start, int& count) {
+  if (c < 3) { start = c; count = 1; }
+  else if (c == 3) { start = 3; count = L - 6; }
+  else { start = L - 7 + c; count = 1; }
+}
+
+template <int M32>
+__global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lc = lane & 31, h = lane >> 5;
+  const int tile = blockIdx.x * 4 + wave;
+  if (tile >= a.tile_start[49]) return;
+  int cls = 0;
+  while (tile >= a.tile_start[cls + 1]) ++cls;
+  const int L = a.L;
+  int y0, ry, x0, rx;
+  class_span(cls / 7, L, y0, ry);
+  class_span(cls % 7, L, x0, rx);
+  const int per = ry * rx, npx = a.F * per;
+  const int base = (tile - a.tile_start[cls]) * 64;
+
+  int py[2], px[2];
+  long xoff[2], ooff[2];
+  bool ok[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int idx = base + nt * 32 + lc;
+    ok[nt] = idx < npx;
+    const int i = ok[nt] ? idx : 0;
+    const int f = i / per, rem = i - f * per;
+    const int iy = rem / rx, ix = rem - iy * rx;
+    const int b = f / a.T, t = f - b * a.T;
+    py[nt] = y0 + iy;
+    px[nt] = x0 + ix;
+    xoff[nt] = (long)b * a.xb + (long)t * a.xt;
+    ooff[nt] = (long)b * a.ob + (long)t * a.ot + (long)py[nt] * L + px[nt];
+  }
+
+  f32x16 acc[M32][2];
+#pragma unroll
+  for (int m = 0; m < M32; ++m)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][nt][r] = 0.f;
+
+  const _Float16* wc = a.w + (long)cls * KSTEPS * M32 * 1024 + lane * 8;
+  int bad = 0;
+  for (int ci = 0; ci < 3; ++ci) {
+    const float* xc = a.x + (long)ci * a.xc;
+#pragma unroll 13
+    for (int dy = 0; dy < 13; ++dy) {
+      const int ks = ci * 13 + dy;
+      h8 ah[M32], al[M32];
+#pragma unroll
+      for (int m = 0; m < M32; ++m) {
+        const _Float16* ap = wc + (long)(ks * M32 + m) * 1024;
+        ah[m] = *reinterpret_cast<const h8*>(ap);
+        al[m] = *reinterpret_cast<const h8*>(ap + 512);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int y = py[nt] + dy - 6;
+        const bool rowok = ok[nt] && y >= 0 && y < L;
+        const float* xr = xc + xoff[nt] + (long)y * L;
+        h8 bh, bl;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int dx = 8 * h + e, xx = px[nt] + dx - 6;
+          float v = 0.f;
+          if (rowok && dx < 13 && xx >= 0 && xx < L) v = xr[xx];
+          v = split_src(v);
+          bad |= fabsf(v) >= 65504.f;
+          const _Float16 hi = (_Float16)v;
+          bh[e] = hi;
+          bl[e] = (_Float16)(v - (float)hi);
+        }
+#pragma unroll
+        for (int m = 0; m < M32; ++m) acc[m][nt] = mma3(ah[m], al[m], bh, bl, acc[m][nt]);
+      }
+    }
+  }
+  if (bad) atomicOr(a.range, 1);
+
+  // ---- epilogue (C/D map: col = lane & 31, row = (r&3) + 8(r>>2) + 4h) ----
+  const float* rs = a.rscale + (long)cls * M32 * 32;
+  const float* cb = a.cbias + (long)cls * M32 * 32;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    if (!ok[nt]) continue;
+#pragma unroll
+    for (int m = 0; m < M32; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < a.Cout) a.out[ooff[nt] + (long)row * a.oc] = acc[m][nt][r] * rs[row] + cb[row];
+      }
+  }
+}
+
+}  // namespace
+
+bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
+                      const float* cbias) {
+  const int L = x.H;
+  if (x.C != 3 || x.W != L || out.H != L || out.W != L || L < 7 || out.C > 64 || out.T != x.T || out.B != x.B)
+    return false;
+  XPathArgs a{};
+  a.x = x.p; a.xb = x.sb; a.xc = x.sc; a.xt = x.st;
+  a.T = x.T; a.L = L; a.F = x.B * x.T;
+  a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
+  a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.cbias = cbias; a.range = x3_range_ptr();
+  a.tile_start[0] = 0;
+  for (int c = 0; c < 49; ++c) {
+    const int cy = c / 7, cx = c % 7;
+    const long n = (long)a.F * (cy == 3 ? L - 6 : 1) * (cx == 3 ? L - 6 : 1);
+    a.tile_start[c + 1] = a.tile_start[c] + (int)((n + 63) / 64);
+  }
+  const unsigned blocks = (unsigned)((a.tile_start[49] + 3) / 4);
+  if (out.C > 32) hipLaunchKernelGGL(xpath_x3_kernel<2>, dim3(blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(xpath_x3_kernel<1>, dim3(blocks), dim3(256), 0, s, a);
+  return true;
+}
+
+}  // namespace extdm

@@ -178,28 +178,42 @@ class NativeWorkload:
                        'rounds': self.rounds, 'parallelism': f'clip-shard x{self.world} (+RCCL all-gather)',
                        'workspace_gb': round(self.h.workspace_bytes() / 2 ** 30, 2)}}
 
+    # extdm_bench_layer ids (runtime.cpp) of the kernels reported, dominant first: the
+    # level-0 ResnetBlock 3x3 conv (64 -> 64 at 32x32, the largest share of GPU time per
+    # step, profiles/r02_*_kernel_stats.csv), init_conv's cond_fea branch (256 -> 64, 7x7;
+    # the x-branch is the composed xpath_x3 kernel) and the level-0 1x1 res_conv (128 -> 64)
+    LAYERS = [(1, 'conv_x3_kernel<3,64,256,1,4,8,2>', 'level-0 ResnetBlock conv 64->64 1x3x3'),
+              (0, 'conv_x3_kernel<7,64,512,1,8,16,1>', 'init_conv cond_fea branch 256->64 1x7x7'),
+              (4, 'conv_x3_kernel<1,64,128,2,4,4,2>', 'level-0 res_conv 128->64 1x1x1')]
+
+    def _traffic(self, layer):
+        """HBM bytes per launch from the committed PMC passes (scripts_gpu/pmc_layers.sh)."""
+        pmc = os.path.join(REPO, 'profiles', f'pmc_layer{layer}.json')
+        try:
+            j = json.load(open(pmc))
+            if int(j.get('batch', -1)) == self.args.batch and j.get('precision') == self.precision:
+                return j.get('hbm_bytes_per_launch')
+        except (ValueError, OSError):
+            pass
+        return None
+
     def roofline(self):
-        """Dominant kernel: init_conv (1x7x7, 512 -> 64), timed with HIP events on
-        the handle's stream over 20 launches of the exact forward launch."""
+        """Per kernel: FLOP per launch / average launch time over 20 launches of the exact
+        forward launch, timed with HIP events on the handle's stream (extdm_bench_layer).
+        The first entry is the dominant kernel; the others ride along under `others`."""
         B = self.args.batch
-        ms_layer, flops = self.h.bench_layer(B, 0, 20)
-        achieved = flops / (ms_layer * 1e-3) / 1e12
-        if self.precision == 'f16x3':
-            kname, peak = 'conv_x3_kernel<7,64,512,1,8,16,1> (init_conv 512->64, 1x7x7, f16x3)', F16X3_PEAK_TFLOPS
-        else:
-            kname, peak = 'conv_halo_kernel<7,64,1,128> (init_conv 512->64, 1x7x7, fp32 MFMA)', FP32_MFMA_PEAK_TFLOPS
-        traffic = None
-        pmc = os.path.join(REPO, 'profiles', 'pmc_init_conv.json')
-        if os.path.exists(pmc):
-            try:
-                j = json.load(open(pmc))
-                if int(j.get('batch', -1)) == B and j.get('precision', 'fp32') == self.precision:
-                    traffic = j.get('hbm_bytes_per_launch')
-            except (ValueError, OSError):
-                traffic = None
-        return {'bound': 'mfma', 'kernel': kname, 'achieved': round(achieved, 2), 'peak': round(peak, 1),
-                'unit': 'TFLOP/s', 'frac': round(achieved / peak, 4), 'traffic': traffic,
-                'launch_ms': round(ms_layer, 4), 'flop_per_launch': flops}
+        peak = F16X3_PEAK_TFLOPS if self.precision == 'f16x3' else FP32_MFMA_PEAK_TFLOPS
+        out = []
+        for layer, kname, what in self.LAYERS:
+            ms_layer, flops = self.h.bench_layer(B, layer, 20)
+            achieved = flops / (ms_layer * 1e-3) / 1e12
+            out.append({'bound': 'mfma', 'kernel': f'{kname} ({what}, {self.precision})',
+                        'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
+                        'frac': round(achieved / peak, 4), 'traffic': self._traffic(layer),
+                        'launch_ms': round(ms_layer, 4), 'flop_per_launch': flops})
+        res = out[0]
+        res['others'] = out[1:]
+        return res
 
     def cpu_baseline(self):
         return cpu_baseline(self.fd, self.rounds, self.args.sampling_steps, self.args.cpu_steps)
