@@ -165,6 +165,16 @@ struct XPathArgs {
 };
 bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
                       const float* cbias);
+// maxpool(1,2,2)(init_noise_conv(x)) in one kernel (xpath_x3.hip): out [B][C][T][L/2][L/2]
+struct NoisePoolArgs {
+  const float* x; long xb, xc, xt;
+  int T, L, F;
+  float* out; long ob, oc, ot; int Cout;
+  const _Float16* w; const float* rscale; const float* bias;
+  int* range;
+};
+bool noise_pool_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
+                           const float* bias);
 bool conv_gemm_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                           int stride, int pad, const ConvEpi& epi);
 void cross_attention(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,

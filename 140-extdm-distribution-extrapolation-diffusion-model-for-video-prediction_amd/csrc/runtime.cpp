@@ -434,6 +434,46 @@ struct ExtdmHandle {
     return xpw;
   }
 
+  // init_noise_conv for the fused conv + maxpool kernel (noise_pool_x3_kernel): A fragments
+  // [kstep = (ci, row pair)][m32][hi|lo][lane][8], k = 8*(lane >> 5) + e -> (dy = 2*pair +
+  // (lane >> 5), dx = e), zero for dy or dx = 7; rows scaled by 2^s(m).
+  XPathW npw;
+  bool noise_pool_ready = false;
+  const XPathW& Pnoise_pool() {
+    if (noise_pool_ready) return npw;
+    const HostTensor& wn = H("init_noise_conv.weight");  // [Cm][3][1][7][7]
+    const int Cm = (int)wn.shape[0], M32 = (Cm + 31) / 32;
+    REQUIRE(wn.shape[1] == 3 && wn.shape.back() == 7, "init_noise_conv: expected a 3 -> C (1,7,7) conv");
+    std::vector<_Float16> g((size_t)12 * M32 * 1024, (_Float16)0.f);
+    std::vector<float> rs(M32 * 32, 0.f);
+    for (int m = 0; m < Cm; ++m) {
+      float mx = 0.f;
+      for (int k = 0; k < 147; ++k) mx = std::max(mx, std::fabs(wn.f[(size_t)m * 147 + k]));
+      int e2 = 0;
+      if (mx > 0.f) { std::frexp(mx, &e2); e2 = 15 - e2; }
+      rs[m] = std::ldexp(1.f, -e2);
+      for (int ci = 0; ci < 3; ++ci)
+        for (int dy = 0; dy < 7; ++dy)
+          for (int dx = 0; dx < 7; ++dx) {
+            const float v = std::ldexp(wn.f[(((size_t)m * 3 + ci) * 7 + dy) * 7 + dx], e2);
+            const int ks = ci * 4 + dy / 2, lane = (m % 32) + 32 * (dy % 2);
+            const size_t base = ((size_t)ks * M32 + m / 32) * 1024;
+            const _Float16 hi = (_Float16)v;
+            g[base + lane * 8 + dx] = hi;
+            g[base + 512 + lane * 8 + dx] = (_Float16)(v - (float)hi);
+          }
+    }
+    npw.w = dmalloc(g.size() * sizeof(_Float16));
+    HIPCHK(hipMemcpy(npw.w, g.data(), g.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    npw.rs = dmalloc(rs.size() * sizeof(float));
+    HIPCHK(hipMemcpy(npw.rs, rs.data(), rs.size() * sizeof(float), hipMemcpyHostToDevice));
+    noise_pool_ready = true;
+    return npw;
+  }
+  bool noise_pool_enabled() const {
+    return xpath_enabled() && cfg.arch == EXTDM_ARCH_U12 && cfg.latent <= 32 && cfg.latent % 2 == 0;
+  }
+
   View alloc_cf(int B, int C, int T, int Hh, int Ww) {
     return cf_view(arena.alloc((size_t)B * C * T * Hh * Ww), B, C, T, Hh, Ww);
   }
@@ -756,7 +796,7 @@ struct ExtdmHandle {
   // TrajWarp (u12:804-827) -> the fused pred-frame features fp' [B,256,tp,fs,fs]
   // TrajWarp (u12:719-827) in two halves. The k / v projections of the cond-frame
   // features fm = cond_fea[:, :, :tc] depend only on cond_fea: trajwarp_kv runs once
-  // per sampling call into the handle's cond cache. trajwarp_q takes x0p, the
+  // per sampling call into the handle's cond cache. trajwarp_q takes the maxpooled
   // init_noise_conv output of the tp predicted frames.
   void trajwarp_kv(const View& fea) {
     const std::string c = "init_traj.cross_att";
@@ -766,12 +806,11 @@ struct ExtdmHandle {
     conv(with_batch(kv_v, fea.B), fm, nullptr, P(c + ".linear_v.weight"), 1, 0, D(c + ".linear_v.bias"), nullptr,
          ACT_RELU);
   }
-  void trajwarp_q(const View& x0p, const View& fea, const View& fp_out) {
+  // xq = maxpool(1,2,2) of the tp frames' init_noise_conv output (u12:811)
+  void trajwarp_q(const View& xq, const View& fea, const View& fp_out) {
     Scope sc(arena);
-    const int B = x0p.B, C = fea.C, tc = cfg.tc, tp = cfg.tp, fs = cfg.fea_size;
-    REQUIRE(x0p.H / 2 == fs && x0p.W / 2 == fs, "TrajWarp: maxpooled latent must match cond_fea size");
-    View xq = alloc_cf(B, x0p.C, tp, fs, fs);
-    if (!plan) maxpool_hw2(s, xq, x0p);
+    const int B = xq.B, C = fea.C, tc = cfg.tc, tp = cfg.tp, fs = cfg.fea_size;
+    REQUIRE(xq.H == fs && xq.W == fs, "TrajWarp: maxpooled latent must match cond_fea size");
     const std::string c = "init_traj.cross_att";
     View q = alloc_cf(B, C, tp, fs, fs);
     conv(q, xq, nullptr, P(c + ".linear_q.weight"), 1, 0, D(c + ".linear_q.bias"), nullptr, ACT_RELU);
@@ -880,14 +919,24 @@ struct ExtdmHandle {
         // the composed x-branch init_conv needs just x itself
         const bool xp = xpath_enabled();
         View x0p;
-        if (arch == EXTDM_ARCH_U12 || !xp) {
+        if (!xp || (arch == EXTDM_ARCH_U12 && !noise_pool_enabled())) {
           x0p = alloc_cf(B, 256, tp, L, L);
           conv(x0p, vx, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
         }
         View fu;
         if (arch == EXTDM_ARCH_U12) {
+          REQUIRE(L / 2 == fs, "TrajWarp: maxpooled latent must match cond_fea size");
+          View xq = alloc_cf(B, 256, tp, fs, fs);
+          if (x0p.p) {
+            if (!plan) maxpool_hw2(s, xq, x0p);
+          } else {
+            const XPathW& nw = Pnoise_pool();
+            if (!plan)
+              REQUIRE(noise_pool_x3_forward(s, xq, vx, nw.w, nw.rs, D("init_noise_conv.bias")),
+                      "fused init_noise_conv + maxpool launch rejected");
+          }
           View fp2 = alloc_cf(B, cfg.fea_ch, tp, fs, fs);
-          trajwarp_q(x0p, vf, fp2);
+          trajwarp_q(xq, vf, fp2);
           fu = alloc_cf(B, cfg.fea_ch, tp, L, L);
           if (!plan) bilinear_frames(s, fu, fp2, fp2, 0);
         } else {

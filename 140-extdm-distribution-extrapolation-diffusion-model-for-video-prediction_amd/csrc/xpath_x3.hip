@@ -39,6 +39,28 @@ __device__ __forceinline__ f32x16 mma3(const h8& ah, const h8& al, const h8& bh,
   return c;
 }
 
+// hi / lo fragments of 8 consecutive columns xs .. xs+7 of row y of an L x L plane, zero
+// outside the plane and for columns e >= ncol. The loads are unconditional (clamped
+// addresses, masked values): exec-masked per-element loads serialised this gather.
+__device__ __forceinline__ void gather8(const float* plane, int y, int xs, int L, int ncol, bool ok, h8& bh, h8& bl,
+                                        int& bad) {
+  const bool rowok = ok && y >= 0 && y < L;
+  const int yc = y < 0 ? 0 : (y >= L ? L - 1 : y);
+  const float* row = plane + (long)yc * L;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int xx = xs + e;
+    const int xc = xx < 0 ? 0 : (xx >= L ? L - 1 : xx);
+    // opaque before the mask, so the load cannot be sunk into a per-element branch
+    const float ld = split_src(row[xc]);
+    const float v = (rowok && e < ncol && xx >= 0 && xx < L) ? ld : 0.f;
+    bad |= fabsf(v) >= 65504.f;
+    const _Float16 hi = (_Float16)v;
+    bh[e] = hi;
+    bl[e] = (_Float16)(v - (float)hi);
+  }
+}
+
 __device__ __forceinline__ void class_span(int c, int L, int& start, int& count) {
   if (c < 3) { start = c; count = 1; }
   else if (c == 3) { start = 3; count = L - 6; }
@@ -50,8 +72,9 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lc = lane & 31, h = lane >> 5;
   const int tile = blockIdx.x * 4 + wave;
   if (tile >= a.tile_start[49]) return;
-  int cls = 0;
-  while (tile >= a.tile_start[cls + 1]) ++cls;
+  int cls = 0;  // static indices: a dynamic index into the kernarg array spills it to scratch
+#pragma unroll
+  for (int c = 1; c < 49; ++c) cls += tile >= a.tile_start[c];
   const int L = a.L;
   int y0, ry, x0, rx;
   class_span(cls / 7, L, y0, ry);
@@ -88,7 +111,7 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
   int bad = 0;
   for (int ci = 0; ci < 3; ++ci) {
     const float* xc = a.x + (long)ci * a.xc;
-#pragma unroll 13
+#pragma unroll 1
     for (int dy = 0; dy < 13; ++dy) {
       const int ks = ci * 13 + dy;
       h8 ah[M32], al[M32];
@@ -98,26 +121,14 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
         ah[m] = *reinterpret_cast<const h8*>(ap);
         al[m] = *reinterpret_cast<const h8*>(ap + 512);
       }
+      h8 bh[2], bl[2];
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int y = py[nt] + dy - 6;
-        const bool rowok = ok[nt] && y >= 0 && y < L;
-        const float* xr = xc + xoff[nt] + (long)y * L;
-        h8 bh, bl;
+      for (int nt = 0; nt < 2; ++nt)
+        gather8(xc + xoff[nt], py[nt] + dy - 6, px[nt] + 8 * h - 6, L, h ? 5 : 8, ok[nt], bh[nt], bl[nt], bad);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int dx = 8 * h + e, xx = px[nt] + dx - 6;
-          float v = 0.f;
-          if (rowok && dx < 13 && xx >= 0 && xx < L) v = xr[xx];
-          v = split_src(v);
-          bad |= fabsf(v) >= 65504.f;
-          const _Float16 hi = (_Float16)v;
-          bh[e] = hi;
-          bl[e] = (_Float16)(v - (float)hi);
-        }
+      for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-        for (int m = 0; m < M32; ++m) acc[m][nt] = mma3(ah[m], al[m], bh, bl, acc[m][nt]);
-      }
+        for (int m = 0; m < M32; ++m) acc[m][nt] = mma3(ah[m], al[m], bh[nt], bl[nt], acc[m][nt]);
     }
   }
   if (bad) atomicOr(a.range, 1);
@@ -138,7 +149,86 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
   }
 }
 
+// TrajWarp's input maxpool(init_noise_conv(x)) (u12:913, 811): the 3 -> C (1,7,7) conv on
+// f16x3 MFMA with the (1,2,2) max pool in the epilogue, so the full-resolution
+// init_noise_conv output never reaches HBM (the composed init_conv no longer reads it).
+// A wave owns two rows 2yp, 2yp+1 of one frame (n-tile nt = row, lane = column, L <= 32)
+// and 4 m32 tiles (128 output channels); K = 3 ch x 4 row pairs x 8 columns (7 used):
+// lane half h takes row 2*dyp + h of the pair. Pool: rows within the lane (nt), columns
+// with the partner lane (lane ^ 1, same rows of the accumulator).
+__global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
+  constexpr int MW = 4;  // m32 tiles per wave
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lc = lane & 31, h = lane >> 5;
+  const int L = a.L, Lh = L / 2;
+  const int nrp = a.F * Lh;
+  const int unit = blockIdx.x * 4 + wave;  // (row pair, m-quarter)
+  const int nmq = (a.Cout + 127) / 128;
+  if (unit >= nrp * nmq) return;
+  const int rp = unit / nmq, mq = unit - rp * nmq;
+  const int f = rp / Lh, yp = rp - f * Lh;
+  const int b = f / a.T, t = f - b * a.T;
+  const bool ok = lc < L;
+  const float* xf = a.x + (long)b * a.xb + (long)t * a.xt;
+
+  f32x16 acc[MW][2];
+#pragma unroll
+  for (int m = 0; m < MW; ++m)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][nt][r] = 0.f;
+  const _Float16* wq = a.w + (long)mq * MW * 1024 + lane * 8;
+  const int M32 = (a.Cout + 31) / 32;
+  int bad = 0;
+#pragma unroll 1
+  for (int ks = 0; ks < 12; ++ks) {
+    const int ci = ks / 4, dy = 2 * (ks % 4) + h;
+    h8 ah[MW], al[MW];
+#pragma unroll
+    for (int m = 0; m < MW; ++m) {
+      const _Float16* ap = wq + (long)(ks * M32 + m) * 1024;
+      ah[m] = *reinterpret_cast<const h8*>(ap);
+      al[m] = *reinterpret_cast<const h8*>(ap + 512);
+    }
+    h8 bh[2], bl[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      gather8(xf + (long)ci * a.xc, 2 * yp + nt + dy - 3, lc - 3, L, dy < 7 ? 7 : 0, ok, bh[nt], bl[nt], bad);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int m = 0; m < MW; ++m) acc[m][nt] = mma3(ah[m], al[m], bh[nt], bl[nt], acc[m][nt]);
+  }
+  if (bad) atomicOr(a.range, 1);
+  float* of = a.out + (long)b * a.ob + (long)t * a.ot + (long)yp * Lh + (lc >> 1);
+#pragma unroll
+  for (int m = 0; m < MW; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (mq * MW + m) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      float v = fmaxf(acc[m][0][r], acc[m][1][r]);
+      v = fmaxf(v, __shfl_xor(v, 1));
+      if (ok && !(lc & 1) && row < a.Cout) of[(long)row * a.oc] = v * a.rscale[row] + a.bias[row];
+    }
+}
+
 }  // namespace
+
+bool noise_pool_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
+                           const float* bias) {
+  const int L = x.H;
+  if (x.C != 3 || x.W != L || L > 32 || (L & 1) || out.H != L / 2 || out.W != L / 2 || out.T != x.T ||
+      out.B != x.B || out.C % 128 != 0)
+    return false;
+  NoisePoolArgs a{};
+  a.x = x.p; a.xb = x.sb; a.xc = x.sc; a.xt = x.st;
+  a.T = x.T; a.L = L; a.F = x.B * x.T;
+  a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
+  a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.bias = bias; a.range = x3_range_ptr();
+  const long units = (long)a.F * (L / 2) * ((out.C + 127) / 128);
+  hipLaunchKernelGGL(noise_pool_x3_kernel, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, s, a);
+  return true;
+}
 
 bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
                       const float* cbias) {
