@@ -45,6 +45,7 @@ struct X3Args {
   const _Float16* w; const float* wscale; int ncgb;
   float* out; long ob, oc, ot; int Cout;
   int TH, NP, nrow_tiles, RS, XPOS;
+  int out_bytes, res_bytes;  // extents of out / e.res (buffer descriptors of the epilogue)
   ConvEpi e;
 };
 
@@ -58,6 +59,20 @@ __device__ __forceinline__ float act_apply(float v, int act) {
   }
 }
 
+// One LDS-DMA piece (16 B per lane, wave-uniform LDS base) issued as inline asm, so that
+// hipcc neither waits for it before the next ordinary global load nor drains it at the
+// next use of one (it does both for __builtin_amdgcn_global_load_lds); the kernel
+// retires it with its own counted vmcnt (cdna_hip_programming.md, LDS-DMA recipe).
+__device__ __forceinline__ void glds16_asm(const void* gsrc, _Float16* lds) {
+  const unsigned dst =
+      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(dst)
+               : "memory");
+}
+
 template <int KS, int BN> struct XMaxX3;
 template <> struct XMaxX3<7, 256> { static constexpr int v = 560; };
 template <> struct XMaxX3<3, 256> { static constexpr int v = 576; };
@@ -66,16 +81,30 @@ template <> struct XMaxX3<1, 128> { static constexpr int v = 128; };
 template <> struct XMaxX3<7, 512> { static constexpr int v = 836; };
 template <> struct XMaxX3<3, 512> { static constexpr int v = 800; };
 
-template <int KS, int BM, int BN, int NG, int WN, int NW, int XBUF>
+// Stage barriers. SPAN = false: __syncthreads() per (channel block, ky) stage. While an
+// A-slot LDS-DMA is in flight its fence waits vmcnt(0), which also drains the X prefetch
+// loads issued in the same stage (65 % of the 1x1 / 52 % of the 3x3 wave cycles were
+// parked there, profiles/r01_pmc_sq_convs_b64.json). SPAN = true: the X loads are issued
+// with an exact count (16 per staging slot, unconditional clamped loads, the value masked
+// by a multiply so hipcc cannot sink a load into a branch), after the stage's A DMA,
+// and each stage ends with `s_waitcnt vmcnt(#X loads) lgkmcnt(0); s_barrier`: the DMA
+// (older) is retired, the X loads (younger) stay in flight into the next stage.
+// NS: staging slots per thread (ceil(XPOS * NG / threads), chosen at launch).
+// KY: ky rows per A slot (stage). KY = KS makes a stage a whole channel block: one
+// barrier per channel block instead of KS, and the X prefetch has all KS*KS*NG MFMA
+// steps to land (the KS consecutive packed slices of a channel block are contiguous).
+template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS>
 __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   constexpr int NT = NW * 64;
   constexpr int PAD = KS / 2;
   constexpr int CIB = 16 * NG;
   constexpr int MT32 = BM / 32;
   constexpr int STEPS = NG * KS;                // per A slot: (g, kx)
-  constexpr int AH = STEPS * MT32 * 2 * 512;    // halves per A slot
-  constexpr int XMAX = XMaxX3<KS, BN>::v;
-  constexpr int NSLOT = (XMAX * NG + NT - 1) / NT;
+  constexpr int AH = STEPS * MT32 * 2 * 512;    // halves per ky slice
+  constexpr int AHS = KY * AH;                  // halves per A slot (stage)
+  constexpr int STG = KS / KY;                  // stages per channel block
+  static_assert(KS % KY == 0, "KY must divide KS");
+  constexpr int NSLOT = NS;
   constexpr int WM = NW / WN;
   constexpr int TM = BM / (32 * WM);
   constexpr int TN = BN / (32 * WN);
@@ -84,8 +113,8 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   extern __shared__ __attribute__((aligned(16))) _Float16 smx[];
   const int XH = a.XPOS * NG * 32;  // halves per X slot (hi + lo)
   _Float16* As0 = smx;
-  _Float16* As1 = smx + AH;
-  _Float16* Xs0 = smx + 2 * AH;
+  _Float16* As1 = smx + AHS;
+  _Float16* Xs0 = smx + 2 * AHS;
   _Float16* Xs1 = XBUF == 2 ? Xs0 + XH : Xs0;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -96,8 +125,8 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   const int row0 = (tile % a.nrow_tiles) * a.TH;
   const int mtile = blockIdx.y;
   const int THK = a.TH + KS - 1;
-  const int NIT = a.ncgb * KS;
-  const _Float16* wt = a.w + (long)mtile * NIT * AH;
+  const int NIT = a.ncgb * STG;
+  const _Float16* wt = a.w + (long)mtile * a.ncgb * KS * AH;
 
   // ---- staging slots: (group, halo position), 16 channels each ----
   int sg[NSLOT], spos[NSLOT], soff0[NSLOT], soff1[NSLOT];
@@ -123,7 +152,52 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   float xr[NSLOT][16];
   int range_bad = 0;
 
-  auto load_x = [&](int cgb) {
+  // plain copies: selecting between fields of the by-value kernarg inside the lambdas
+  // made hipcc spill the whole X3Args to scratch
+  const float* const gin0 = a.in0;
+  const float* const gin1 = a.in1;
+  const long gi0c = a.i0c, gi1c = a.i1c;
+  const int gC0 = a.C0, gCin = a.Cin;
+  // channel groups never straddle the two sources nor run past Cin (wave-uniform)
+  const bool whole = gC0 % 16 == 0 && gCin % CIB == 0;
+  auto load_x_exact = [&](int cgb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < NSLOT; ++j) {  // every slot loads (unused ones a masked dummy): 16 * NSLOT loads
+      const bool pos_ok = soff0[j] >= 0;
+      const int o0 = pos_ok ? soff0[j] : 0, o1 = pos_ok ? soff1[j] : 0;
+      const int ci0 = cgb * CIB + (sg[j] < 0 ? 0 : sg[j]) * 16;
+      // raw values only: any use of a load result here (even the mask) makes hipcc wait
+      // vmcnt(0) while the stage's A DMA is in flight; store_x masks them
+      if (whole) {
+        const bool s1 = ci0 >= gC0;
+        const float* bp = s1 ? gin1 + (long)(ci0 - gC0) * gi1c + o1 : gin0 + (long)ci0 * gi0c + o0;
+        const long cs = s1 ? gi1c : gi0c;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) xr[j][c] = bp[c * cs];
+        continue;
+      }
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int ci = ci0 + c;
+        const bool s1 = ci >= gC0;
+        int cc = s1 ? ci - gC0 : ci;
+        const int cmax = s1 ? gCin - gC0 - 1 : gC0 - 1;
+        cc = cc > cmax ? cmax : cc;
+        const long off = s1 ? (long)cc * gi1c + o1 : (long)cc * gi0c + o0;
+        xr[j][c] = (s1 ? gin1 : gin0)[off];
+      }
+    }
+  };
+  // store-time mask of an exact-count slot: halo position inside the image, channel < Cin
+  auto xmask = [&](int j, int cgb, int c) __attribute__((always_inline)) {
+    const int ci = cgb * CIB + (sg[j] < 0 ? 0 : sg[j]) * 16 + c;
+    return (soff0[j] >= 0 && ci < gCin) ? 1.f : 0.f;
+  };
+  auto load_x = [&](int cgb) __attribute__((always_inline)) {
+    if (SPAN) {
+      load_x_exact(cgb);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < NSLOT; ++j) {
       const int ci0 = cgb * CIB + sg[j] * 16;
@@ -150,14 +224,27 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   };
   // 16-byte chunk h of position pos sits at chunk h ^ bit3(pos): conflict-free
   // ds_read_b128 for 32 consecutive positions (lane groups of 16, MI355X_MICROARCH §LDS)
-  auto store_x = [&](_Float16* Xs) {
+  // An unused slot (SPAN) stores its zeros into a 64-byte dummy past the X buffers
+  // instead of branching around the store: a lane-divergent skip leaves the X loads
+  // pending on one path, and hipcc's path-insensitive wait analysis then drains vmcnt(0)
+  // at the next channel block's X prefetch.
+  _Float16* const xdummy = Xs0 + XBUF * XH;  // 32 halves, then the epilogue's scale/bias rows
+  auto store_x = [&](_Float16* Xs, int cgb) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < NSLOT; ++j) {
-      if (sg[j] < 0) continue;
+      if (!SPAN && sg[j] < 0) continue;
       h8 hi0, hi1, lo0, lo1;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const float v0 = split_src(xr[j][c]), v1 = split_src(xr[j][c + 8]);
+        const float m0 = SPAN ? xmask(j, cgb, c) : 1.f, m1 = SPAN ? xmask(j, cgb, c + 8) : 1.f;
+        float r0 = xr[j][c], r1 = xr[j][c + 8];
+        if (SPAN) {
+          // pinned here (volatile: not hoisted above the stage barriers of the 7x7
+          // ky loop, where the first use of a load result would wait for the X loads)
+          asm volatile("" : "+v"(r0));
+          asm volatile("" : "+v"(r1));
+        }
+        const float v0 = split_src(r0 * m0), v1 = split_src(r1 * m1);
         range_bad |= (fabsf(v0) >= 65504.f) | (fabsf(v1) >= 65504.f);
         const _Float16 a0 = (_Float16)v0, a1 = (_Float16)v1;
         hi0[c] = a0; hi1[c] = a1;
@@ -165,21 +252,25 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
         lo1[c] = (_Float16)(v1 - (float)a1);
       }
       const int sw = (spos[j] >> 3) & 1;
-      _Float16* dh = Xs + ((long)sg[j] * a.XPOS + spos[j]) * 16;
-      _Float16* dl = dh + (long)NG * a.XPOS * 16;
+      const bool used = sg[j] >= 0;
+      _Float16* dh = used ? Xs + ((long)sg[j] * a.XPOS + spos[j]) * 16 : xdummy;
+      _Float16* dl = used ? dh + (long)NG * a.XPOS * 16 : xdummy + 16;
       *reinterpret_cast<h8*>(dh + 8 * sw) = hi0;
       *reinterpret_cast<h8*>(dh + 8 * (sw ^ 1)) = hi1;
       *reinterpret_cast<h8*>(dl + 8 * sw) = lo0;
       *reinterpret_cast<h8*>(dl + 8 * (sw ^ 1)) = lo1;
     }
   };
-  constexpr int NPIECE = AH / 512;  // 1 KiB pieces
+  constexpr int NPIECE = AHS / 512;  // 1 KiB pieces
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   auto load_a = [&](int it, _Float16* As) {
-    const _Float16* src = wt + (long)it * AH;
-    for (int pc = wave_u; pc < NPIECE; pc += NW)
-      __builtin_amdgcn_global_load_lds((const void*)(src + pc * 512 + lane * 8), (lds_ptr_t)(As + pc * 512), 16, 0,
-                                       0);
+    const _Float16* src = wt + (long)it * AHS;
+    for (int pc = wave_u; pc < NPIECE; pc += NW) {
+      if (SPAN) glds16_asm(src + pc * 512 + lane * 8, As + pc * 512);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)(src + pc * 512 + lane * 8), (lds_ptr_t)(As + pc * 512), 16, 0,
+                                         0);
+    }
   };
 
   // ---- per-lane operand bases ----
@@ -201,17 +292,38 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // per-row output scale and bias of this m-tile, staged for the epilogue
+  float* const ep_sc = reinterpret_cast<float*>(xdummy + 32);
+  float* const ep_bi = ep_sc + BM;
+  if (tid < BM) {
+    const int m = mtile * BM + tid;
+    const int mc = m < a.Cout ? m : a.Cout - 1;
+    ep_sc[tid] = a.wscale[mc];
+    ep_bi[tid] = a.e.bias ? a.e.bias[mc] : 0.f;
+  }
   load_x(0);
   load_a(0, As0);
-  store_x(Xs0);
-  __syncthreads();
-  for (int it = 0; it < NIT; ++it) {
-    const int cgb = it / KS, ky = it - cgb * KS;
-    const _Float16* As = (it & 1) ? As1 : As0;
+  store_x(Xs0, 0);
+  if (SPAN) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the asm DMA is invisible to __syncthreads
+  else __syncthreads();
+  // One (channel block, ky block) stage. `more` = a next channel block exists (its X is
+  // prefetched at stage 0 and stored at stage STG - 1). The stages of a channel block are
+  // issued as stage 0 peeled + the rest, and the last channel block is peeled with
+  // more = false, so that hipcc sees the X prefetch and its store_x in one region with no
+  // X load pending across a loop back edge (a path-insensitive pending load there made it
+  // wait vmcnt(0) before re-loading the xr registers, right behind the stage's A DMA).
+  auto stage = [&](int cgb, int kb, bool more) __attribute__((always_inline)) {
+    const int it = cgb * STG + kb;
+    const _Float16* Ast = (it & 1) ? As1 : As0;
     const _Float16* Xs = (cgb & 1) ? Xs1 : Xs0;
     if (it + 1 < NIT) load_a(it + 1, (it & 1) ? As0 : As1);
-    const bool pre = (ky == 0) && (cgb + 1 < a.ncgb);
+    const bool pre = (kb == 0) && more;
+    if (SPAN) __builtin_amdgcn_sched_barrier(0);  // the X loads issue after the DMA (vmcnt order)
     if (pre) load_x(cgb + 1);
+#pragma unroll
+    for (int kyl = 0; kyl < KY; ++kyl) {
+    const int ky = kb * KY + kyl;
+    const _Float16* As = Ast + kyl * AH;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
 #pragma unroll
@@ -241,59 +353,150 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
           }
       }
     }
-    if (ky == KS - 1 && cgb + 1 < a.ncgb) {
-      if (XBUF == 1) __syncthreads();  // single X buffer: every wave is done with it
-      store_x((cgb & 1) ? Xs0 : Xs1);
     }
-    __syncthreads();
-  }
+    if (kb == STG - 1 && more) {
+      if (XBUF == 1) {  // single X buffer: every wave is done with it
+        if (SPAN) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else __syncthreads();
+      }
+      store_x((cgb & 1) ? Xs0 : Xs1, cgb + 1);
+    }
+    if (SPAN) {
+      // retire this stage's A DMA (issued before the X prefetch) and this wave's LDS
+      // writes; the prefetch loads (16 per slot) may stay in flight across the barrier
+      // (only at ky = 0: a later stage's DMA is younger than the X loads, and vmcnt
+      // retires in issue order, so waiting for it is vmcnt(0))
+      if (pre && STG > 1) {
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(16 * NSLOT) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+    } else {
+      __syncthreads();
+    }
+  };
+  auto channel_block = [&](int cgb, bool more) __attribute__((always_inline)) {
+    stage(cgb, 0, more);
+    if (STG > 3) {
+#pragma unroll 1
+      for (int kb = 1; kb < STG; ++kb) stage(cgb, kb, more);
+    } else {
+#pragma unroll
+      for (int kb = 1; kb < STG; ++kb) stage(cgb, kb, more);
+    }
+  };
+  for (int cgb = 0; cgb + 1 < a.ncgb; ++cgb) channel_block(cgb, true);
+  channel_block(a.ncgb - 1, false);
   if (range_bad) atomicOr(&g_x3_range, 1);
 
   // ---- epilogue (C/D map: col = lane & 31, row = (r&3) + 8(r>>2) + 4h) ----
+  // Every operand load of a row group is issued before its first use (clamped indices,
+  // kernel-uniform branches only): per-element guarded loads made hipcc wait for each
+  // one in turn, ~32 serial L2 round trips per wave at one workgroup per CU.
+  const bool has_res = a.e.res != nullptr;
+  const bool has_post = a.e.post_scale != nullptr, post_pc = a.e.post_per_channel != 0;
+  const int act = a.e.act;
+  const auto rs_out = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.out_bytes, 0x00020000);
+  const auto rs_res = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.e.res), 0, a.res_bytes, 0x00020000);
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = (wn * TN + j) * 32 + lc;
-    const int p = n / (a.TH * a.W);
-    const int r = (n / a.W) % a.TH;
-    const int c = n % a.W;
-    const int q = plane0 + p, row = row0 + r;
-    if (q >= a.P || row >= a.H) continue;
-    const int b = q / a.T, t = q - b * a.T;
-    const long pix = (long)row * a.W + c;
-    const long obase = (long)b * a.ob + (long)t * a.ot + pix;
-    const long rbase = (long)b * a.e.res_sb + (long)t * a.e.res_st + pix;
+  for (int i = 0; i < TM; ++i) {
+    int mrow[16];
+    float scl[16], bia[16];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int k = 0; k < 4; ++k) {
+      const int ml = (wm * TM + i) * 32 + 8 * k + 4 * h;  // rows ml .. ml + 3 of the tile
+      const float4 s4 = *reinterpret_cast<const float4*>(ep_sc + ml);
+      const float4 b4 = *reinterpret_cast<const float4*>(ep_bi + ml);
+      scl[4 * k] = s4.x; scl[4 * k + 1] = s4.y; scl[4 * k + 2] = s4.z; scl[4 * k + 3] = s4.w;
+      bia[4 * k] = b4.x; bia[4 * k + 1] = b4.y; bia[4 * k + 2] = b4.z; bia[4 * k + 3] = b4.w;
+    }
+#pragma unroll
+    for (int r16 = 0; r16 < 16; ++r16) {
+      const int m = mtile * BM + (wm * TM + i) * 32 + (r16 & 3) + 8 * (r16 >> 2) + 4 * h;
+      mrow[r16] = m < a.Cout ? m : a.Cout - 1;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = (wn * TN + j) * 32 + lc;
+      const int p = n / (a.TH * a.W);
+      const int r = (n / a.W) % a.TH;
+      const int c = n % a.W;
+      const int q0 = plane0 + p, row0q = row0 + r;
+      const bool valid = q0 < a.P && row0q < a.H;
+      const int q = valid ? q0 : 0, row = valid ? row0q : 0;
+      const int b = q / a.T, t = q - b * a.T;
+      const int pix = row * a.W + c;
+      float v[16];
+#pragma unroll
+      for (int r16 = 0; r16 < 16; ++r16) v[r16] = acc[i][j][r16] * scl[r16] + bia[r16];
+      if (has_res) {
+        const int rbase = (int)((long)b * a.e.res_sb + (long)t * a.e.res_st) + pix;
+        float rv[16];
+#pragma unroll
+        for (int r16 = 0; r16 < 16; ++r16)
+          rv[r16] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+              rs_res, (rbase + mrow[r16] * (int)a.e.res_sc) * 4, 0, 0));
+#pragma unroll
+        for (int r16 = 0; r16 < 16; ++r16) v[r16] += rv[r16];
+      }
+      if (has_post) {
+        float ps[16], pt[16];
+#pragma unroll
+        for (int r16 = 0; r16 < 16; ++r16) {
+          const int pi = post_pc ? mrow[r16] : b * a.Cout + mrow[r16];
+          ps[r16] = a.e.post_scale[pi];
+          pt[r16] = a.e.post_shift[pi];
+        }
+#pragma unroll
+        for (int r16 = 0; r16 < 16; ++r16) v[r16] = v[r16] * ps[r16] + pt[r16];
+      }
+      if (act != ACT_NONE) {
+#pragma unroll
+        for (int r16 = 0; r16 < 16; ++r16) v[r16] = act_apply(v[r16], act);
+      }
+      // 32-bit byte offsets into a bounded descriptor; a lane outside the image or a row
+      // past Cout stores to an offset past the extent, which the range check drops
+      const int obase = (int)((long)b * a.ob + (long)t * a.ot) + pix;
 #pragma unroll
       for (int r16 = 0; r16 < 16; ++r16) {
         const int m = mtile * BM + (wm * TM + i) * 32 + (r16 & 3) + 8 * (r16 >> 2) + 4 * h;
-        if (m >= a.Cout) continue;
-        float v = acc[i][j][r16] * a.wscale[m];
-        if (a.e.bias) v += a.e.bias[m];
-        if (a.e.res) v += a.e.res[rbase + (long)m * a.e.res_sc];
-        if (a.e.post_scale) {
-          const long pi = a.e.post_per_channel ? (long)m : (long)b * a.Cout + m;
-          v = v * a.e.post_scale[pi] + a.e.post_shift[pi];
-        }
-        v = act_apply(v, a.e.act);
-        a.out[obase + (long)m * a.oc] = v;
+        const int off = (valid && m < a.Cout) ? (obase + m * (int)a.oc) * 4 : a.out_bytes;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r16]), rs_out, off, 0, 0);
       }
     }
   }
 }
 
-template <int KS, int BM, int BN, int NG, int WN, int NW, int XBUF>
-void launch(hipStream_t s, const X3Args& a, unsigned ntiles) {
-  constexpr int AH = NG * KS * (BM / 32) * 2 * 512;
-  const size_t lds = ((size_t)2 * AH + (size_t)XBUF * a.XPOS * NG * 32) * sizeof(_Float16);
+template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS>
+void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
+  constexpr int AH = KY * NG * KS * (BM / 32) * 2 * 512;
+  // + 32 halves (unused-slot dummy) + 2 * BM floats (epilogue scale / bias)
+  const size_t lds = ((size_t)2 * AH + (size_t)XBUF * a.XPOS * NG * 32 + 32 + 4 * BM) * sizeof(_Float16);
   dim3 grid(ntiles, (a.Cout + BM - 1) / BM);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, BM, BN, NG, WN, NW, XBUF>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_x3_kernel<KS, BM, BN, NG, WN, NW, XBUF>), grid, dim3(NW * 64), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS>), grid, dim3(NW * 64), lds, s, a);
+}
+
+template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN>
+void launch_ns(hipStream_t s, const X3Args& a, unsigned ntiles) {
+  constexpr int XMAX = XMaxX3<KS, BN>::v;
+  static_assert((XMAX * NG + NW * 64 - 1) / (NW * 64) <= 2, "more than two staging slots");
+  if constexpr (XMAX * NG <= NW * 64) launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 1>(s, a, ntiles);
+  else if (a.XPOS * NG <= NW * 64) launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 1>(s, a, ntiles);
+  else launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 2>(s, a, ntiles);
+}
+
+template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF>
+void launch(hipStream_t s, const X3Args& a, unsigned ntiles) {
+  // EXTDM_X3_NOSPAN=1: per-stage __syncthreads() (A/B against the spanning barriers)
+  static const bool nospan = [] { const char* v = getenv("EXTDM_X3_NOSPAN"); return v && v[0] && v[0] != '0'; }();
+  if (nospan) launch_ns<KS, KY, BM, BN, NG, WN, NW, XBUF, false>(s, a, ntiles);
+  else launch_ns<KS, KY, BM, BN, NG, WN, NW, XBUF, true>(s, a, ntiles);
 }
 
 }  // namespace
@@ -337,18 +540,27 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
   a.nrow_tiles = (H + a.TH - 1) / a.TH;
   a.e = epi;
+  // the epilogue addresses out / res with 32-bit byte offsets (buffer descriptors)
+  auto extent = [&](long sb, long sc, long st, int C) {
+    return ((long)(out.B - 1) * sb + (long)(C - 1) * sc + (long)(out.T - 1) * st + (long)H * W) * 4;
+  };
+  const long ob = extent(out.sb, out.sc, out.st, out.C);
+  const long rb = epi.res ? extent(epi.res_sb, epi.res_sc, epi.res_st, out.C) : 0;
+  if (ob >= (1L << 31) - 4 || rb >= (1L << 31) - 4) return false;
+  a.out_bytes = (int)ob;
+  a.res_bytes = (int)rb;
   const unsigned ntiles = (unsigned)(((a.P + a.NP - 1) / a.NP) * a.nrow_tiles);
   if (tl.bn == 512) {
-    if (ks == 7 && tl.bm == 64) launch<7, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
-    else if (ks == 3 && tl.bm == 64) launch<3, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
+    if (ks == 7 && tl.bm == 64) launch<7, 1, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
+    else if (ks == 3 && tl.bm == 64) launch<3, 1, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
     else return false;
     return true;
   }
-  if (ks == 7 && tl.bm == 64) launch<7, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
-  else if (ks == 3 && tl.bm == 64) launch<3, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
-  else if (ks == 3 && tl.bm == 128) launch<3, 128, 128, 1, 2, 8, 2>(s, a, ntiles);
-  else if (ks == 1 && tl.bm == 64) launch<1, 64, 128, 2, 4, 4, 2>(s, a, ntiles);
-  else if (ks == 1 && tl.bm == 128) launch<1, 128, 128, 2, 2, 4, 2>(s, a, ntiles);
+  if (ks == 7 && tl.bm == 64) launch<7, 1, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
+  else if (ks == 3 && tl.bm == 64) launch<3, 3, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
+  else if (ks == 3 && tl.bm == 128) launch<3, 1, 128, 128, 1, 2, 8, 2>(s, a, ntiles);
+  else if (ks == 1 && tl.bm == 64) launch<1, 1, 64, 128, 2, 4, 4, 2>(s, a, ntiles);
+  else if (ks == 1 && tl.bm == 128) launch<1, 1, 128, 128, 2, 2, 4, 2>(s, a, ntiles);
   else return false;
   return true;
 }
