@@ -233,14 +233,18 @@ void launch_bm(hipStream_t s, const ConvArgs& a, int bm, dim3 grid_n) {
 
 }  // namespace
 
-void conv_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
-                  int stride, int pad, const ConvEpi& epi) {
-  if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 && conv_x3_forward(s, out, in0, in1, w, epi))
-    return;
-  if (conv_gemm_x3_forward(s, out, in0, in1, w, stride, pad, epi)) return;
+int conv_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
+                 int stride, int pad, const ConvEpi& epi_in) {
+  int slots = 0;
+  if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 &&
+      conv_x3_forward(s, out, in0, in1, w, epi_in, &slots))
+    return slots;
+  ConvEpi epi = epi_in;  // the other paths leave the statistics to the caller
+  epi.stats = nullptr;
+  if (conv_gemm_x3_forward(s, out, in0, in1, w, stride, pad, epi)) return 0;
   if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 && !getenv_flag("EXTDM_NO_HALO") &&
       conv_halo_forward(s, out, in0, in1, w, epi))
-    return;
+    return 0;
   ConvArgs a{};
   a.in0 = in0.p; a.i0b = in0.sb; a.i0c = in0.sc; a.i0t = in0.st;
   a.C0 = in0.C;
@@ -259,12 +263,13 @@ void conv_forward(hipStream_t s, const View& out, const View& in0, const View* i
   const int bm = conv_bm(w.M);  // the packer padded Mpad to a multiple of this tile
   dim3 gn((unsigned)((a.N + BN - 1) / BN), 1, w.mode == MODE_DECONV ? 4 : 1);
   const int kh = w.KH, kw = w.KW;
-  if (w.mode == MODE_DECONV) { launch_bm<2, 2, MODE_DECONV>(s, a, bm, gn); return; }
-  if (w.mode == MODE_UP2) { launch_bm<3, 3, MODE_UP2>(s, a, bm, gn); return; }
+  if (w.mode == MODE_DECONV) { launch_bm<2, 2, MODE_DECONV>(s, a, bm, gn); return 0; }
+  if (w.mode == MODE_UP2) { launch_bm<3, 3, MODE_UP2>(s, a, bm, gn); return 0; }
   if (kh == 1 && kw == 1) launch_bm<1, 1, MODE_CONV>(s, a, bm, gn);
   else if (kh == 3 && kw == 3) launch_bm<3, 3, MODE_CONV>(s, a, bm, gn);
   else if (kh == 4 && kw == 4) launch_bm<4, 4, MODE_CONV>(s, a, bm, gn);
   else if (kh == 7 && kw == 7) launch_bm<7, 7, MODE_CONV>(s, a, bm, gn);
+  return 0;
 }
 
 }  // namespace extdm

@@ -46,6 +46,7 @@ struct X3Args {
   float* out; long ob, oc, ot; int Cout;
   int TH, NP, nrow_tiles, RS, XPOS;
   int out_bytes, res_bytes;  // extents of out / e.res (buffer descriptors of the epilogue)
+  int stats_split;           // GroupNorm partial slots per (b, group) when e.stats is set
   ConvEpi e;
 };
 
@@ -396,12 +397,18 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   const bool has_res = a.e.res != nullptr;
   const bool has_post = a.e.post_scale != nullptr, post_pc = a.e.post_per_channel != 0;
   const int act = a.e.act;
+  // GroupNorm statistics of the stored values, per 8-row block (i, k) of the lane's rows
+  // (r16 = 4k .. 4k + 3 on both halves h): fp32 within the lane, pairwise across lanes,
+  // double across waves and into the (b, group) partial of this tile
+  const bool do_stats = a.e.stats != nullptr;
+  float* const red = reinterpret_cast<float*>(smx);  // [wave][TM * 4][2]; A / X staging is dead here
   const auto rs_out = __builtin_amdgcn_make_buffer_rsrc(a.out, 0, a.out_bytes, 0x00020000);
   const auto rs_res = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.e.res), 0, a.res_bytes, 0x00020000);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     int mrow[16];
     float scl[16], bia[16];
+    float st_s[4] = {0.f, 0.f, 0.f, 0.f}, st_q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int ml = (wm * TM + i) * 32 + 8 * k + 4 * h;  // rows ml .. ml + 3 of the tile
@@ -460,8 +467,53 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
 #pragma unroll
       for (int r16 = 0; r16 < 16; ++r16) {
         const int m = mtile * BM + (wm * TM + i) * 32 + (r16 & 3) + 8 * (r16 >> 2) + 4 * h;
-        const int off = (valid && m < a.Cout) ? (obase + m * (int)a.oc) * 4 : a.out_bytes;
+        const bool ok = valid && m < a.Cout;
+        const int off = ok ? (obase + m * (int)a.oc) * 4 : a.out_bytes;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r16]), rs_out, off, 0, 0);
+        if (do_stats) {
+          const float x = ok ? v[r16] : 0.f;
+          st_s[r16 >> 2] += x;
+          st_q[r16 >> 2] += x * x;
+        }
+      }
+    }
+    if (do_stats) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float s_ = st_s[k], q_ = st_q[k];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          s_ += __shfl_xor(s_, off);
+          q_ += __shfl_xor(q_, off);
+        }
+        if (lane == 0) {
+          red[(wave * TM * 4 + i * 4 + k) * 2] = s_;
+          red[(wave * TM * 4 + i * 4 + k) * 2 + 1] = q_;
+        }
+      }
+    }
+  }
+  if (do_stats) {
+    __syncthreads();
+    const int G = a.e.stats_groups, Cg = a.Cout / G;
+    const int ngrp = BM / Cg;  // groups of this m-tile (host: Cg % 8 == 0, BM % Cg == 0)
+    if (tid < ngrp) {
+      const int g = mtile * ngrp + tid;
+      if (g < G) {
+        double s_ = 0.0, q_ = 0.0;
+        for (int kb = tid * (Cg / 8); kb < (tid + 1) * (Cg / 8); ++kb) {  // 8-row blocks of the group
+          const int wmk = kb / (TM * 4), ik = kb % (TM * 4);
+          for (int wn_ = 0; wn_ < WN; ++wn_) {
+            const int w_ = wmk * WN + wn_;
+            s_ += (double)red[(w_ * TM * 4 + ik) * 2];
+            q_ += (double)red[(w_ * TM * 4 + ik) * 2 + 1];
+          }
+        }
+        const int bq = plane0 / a.T;  // the tile's sample (host: T % NP == 0)
+        const int slot = ((plane0 % a.T) / a.NP) * a.nrow_tiles + tile % a.nrow_tiles;
+        double* pp = a.e.stats + (((long)bq * G + g) * a.stats_split + slot) * 2;
+        pp[0] = s_;
+        pp[1] = q_;
       }
     }
   }
@@ -485,10 +537,18 @@ void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN>
 void launch_ns(hipStream_t s, const X3Args& a, unsigned ntiles) {
   constexpr int XMAX = XMaxX3<KS, BN>::v;
-  static_assert((XMAX * NG + NW * 64 - 1) / (NW * 64) <= 2, "more than two staging slots");
-  if constexpr (XMAX * NG <= NW * 64) launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 1>(s, a, ntiles);
-  else if (a.XPOS * NG <= NW * 64) launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 1>(s, a, ntiles);
-  else launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 2>(s, a, ntiles);
+  constexpr int NT = NW * 64;
+  static_assert((XMAX * NG + NT - 1) / NT <= 3, "more than three staging slots");
+  const int need = (a.XPOS * NG + NT - 1) / NT;
+  if constexpr (XMAX * NG <= NT) launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 1>(s, a, ntiles);
+  else if constexpr (XMAX * NG <= 2 * NT) {
+    if (need <= 1) launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 1>(s, a, ntiles);
+    else launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 2>(s, a, ntiles);
+  } else {
+    if (need <= 1) launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 1>(s, a, ntiles);
+    else if (need == 2) launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 2>(s, a, ntiles);
+    else launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 3>(s, a, ntiles);
+  }
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF>
@@ -516,7 +576,8 @@ X3Tile x3_tile(int ks, int cout) {
 }
 
 bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
-                     const ConvEpi& epi) {
+                     const ConvEpi& epi, int* stats_slots) {
+  if (stats_slots) *stats_slots = 0;
   if (!w.wx || w.mode != MODE_CONV) return false;
   const int ks = w.KH;
   const int H = in0.H, W = in0.W;
@@ -549,6 +610,20 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   if (ob >= (1L << 31) - 4 || rb >= (1L << 31) - 4) return false;
   a.out_bytes = (int)ob;
   a.res_bytes = (int)rb;
+  // GroupNorm partials in the epilogue: whole tiles inside one sample, groups of whole
+  // 8-row blocks inside one m-tile, at most 64 slots (the runtime's partials buffer)
+  if (epi.stats) {
+    const int G = epi.stats_groups, Cg = G > 0 ? out.C / G : 0;
+    const int split = (out.T / std::max(a.NP, 1)) * a.nrow_tiles;
+    const bool ok = G > 0 && out.C % G == 0 && Cg % 8 == 0 && tl.bm % Cg == 0 && out.T % a.NP == 0 &&
+                    split >= 1 && split <= 64;
+    if (ok) {
+      a.stats_split = split;
+      if (stats_slots) *stats_slots = split;
+    } else {
+      a.e.stats = nullptr;
+    }
+  }
   const unsigned ntiles = (unsigned)(((a.P + a.NP - 1) / a.NP) * a.nrow_tiles);
   if (tl.bn == 512) {
     if (ks == 7 && tl.bm == 64) launch<7, 1, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
@@ -557,7 +632,15 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     return true;
   }
   if (ks == 7 && tl.bm == 64) launch<7, 1, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
-  else if (ks == 3 && tl.bm == 64) launch<3, 3, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
+  else if (ks == 3 && tl.bm == 64) {
+    // EXTDM_X3_V3=1: the 8-wave tile (32 x 64 per wave, whole-channel-block stages, one
+    // workgroup per CU at 117 KB of LDS). Default: 4 waves of 64 x 64 (12 MFMAs per 8
+    // ds_read_b128 instead of 6 per 6) at 68 KB, two independent workgroups per CU,
+    // 12 % faster on the level-0 64 -> 64 conv at B = 64.
+    static const int v3 = [] { const char* v = getenv("EXTDM_X3_V3"); return v ? atoi(v) : 0; }();
+    if (v3 == 1) launch<3, 3, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
+    else launch<3, 1, 64, 256, 1, 4, 4, 2>(s, a, ntiles);
+  }
   else if (ks == 3 && tl.bm == 128) launch<3, 1, 128, 128, 1, 2, 8, 2>(s, a, ntiles);
   else if (ks == 1 && tl.bm == 64) launch<1, 1, 64, 128, 2, 4, 4, 2>(s, a, ntiles);
   else if (ks == 1 && tl.bm == 128) launch<1, 1, 128, 128, 2, 2, 4, 2>(s, a, ntiles);

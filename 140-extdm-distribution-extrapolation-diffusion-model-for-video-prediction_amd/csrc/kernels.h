@@ -77,6 +77,10 @@ struct ConvEpi {
   const float* post_shift = nullptr;
   int post_per_channel = 0;
   int act = ACT_NONE;
+  // GroupNorm statistics of the output (the conv's epilogue computes them where the
+  // kernel supports it): partials [b * stats_groups + g][slot][2] = (sum, sum of squares)
+  double* stats = nullptr;
+  int stats_groups = 0;
 };
 
 // Input channels per half-stage of the halo conv for kernel size ks and tile bm.
@@ -89,21 +93,26 @@ bool conv_halo_forward(hipStream_t s, const View& out, const View& in0, const Vi
 // the geometry is not covered), and the activation-range flag (|v| >= 65504 seen).
 struct X3Tile { int bm, bn, ng; };
 X3Tile x3_tile(int ks, int cout);
+// With epi.stats set, *stats_slots receives the number of partial slots per (b, group)
+// the epilogue wrote (0: not computed, the caller runs the statistics pass).
 bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
-                     const ConvEpi& epi);
+                     const ConvEpi& epi, int* stats_slots = nullptr);
 void x3_range_reset(hipStream_t s);
 int* x3_range_ptr();  // device address of the flag on the current device
 int x3_range_read(hipStream_t s);
 
 // out = act(conv(in0 ++ in1) + bias + res) [* s + sh]
-void conv_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
-                  int stride, int pad, const ConvEpi& epi);
+// Returns the GroupNorm partial slots written for epi.stats (0 if none).
+int conv_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
+                 int stride, int pad, const ConvEpi& epi);
 
 // GroupNorm(G) over a channel-first view, optional FiLM (x*(scale+1)+shift from
 // a [Mtot][NT] table at row offset, column t[b]) then SiLU, optional residual.
 void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, const float* gamma,
                     const float* beta, const float* film, int film_row, int film_nt, const int* t_batch,
-                    const View* res, double* partials);
+                    const View* res, double* partials, int given_split = 0);
+// given_split > 0: `partials` already holds that many (sum, sumsq) slots per (b, group)
+// (written by the producing conv's epilogue); the statistics pass is skipped.
 
 // Channel LayerNorm (biased var over C, gamma only; u12:138-147) of in0 ++ in1.
 void channel_ln(hipStream_t s, const View& out, const View& in0, const View* in1, const float* gamma);

@@ -598,7 +598,7 @@ inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
 void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, const float* gamma,
                     const float* beta, const float* film, int film_row, int film_nt, const int* t_batch,
-                    const View* res, double* partials) {
+                    const View* res, double* partials, int given_split) {
   // the statistics kernels read each (b, group) as Cg*T*H*W contiguous floats
   if (x.st != x.HW() || x.sc != (long)x.T * x.HW() || x.C % groups != 0)
     throw std::invalid_argument("groupnorm_silu: input must be [B][C][T][H][W] with contiguous (C, T, H, W) "
@@ -609,7 +609,9 @@ void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, c
   if (split < 1) split = 1;
   if (split > 64) split = 64;
   auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (L % 4 == 0 && al16(x.p) && x.sb % 4 == 0 && x.sc % 4 == 0) {
+  if (given_split > 0) {
+    split = given_split;  // the producing conv's epilogue wrote the partials
+  } else if (L % 4 == 0 && al16(x.p) && x.sb % 4 == 0 && x.sc % 4 == 0) {
     // ~8 float4 loads per thread per block, at most 64 blocks per group (partials size)
     long chunk = (L + 63) / 64;
     if (chunk < 8192) chunk = 8192;

@@ -101,6 +101,8 @@ struct ExtdmHandle {
   // workspace
   Arena arena;
   double* partials = nullptr;
+  // EXTDM_NO_GN_FUSE=1: separate GroupNorm statistics pass after every ResnetBlock conv
+  const bool fuse_gn_stats = [] { const char* v = getenv("EXTDM_NO_GN_FUSE"); return !(v && v[0] && v[0] != '0'); }();
   int* t_batch = nullptr;
   int* step_ctr = nullptr;
   StepCoef* coefs = nullptr;
@@ -482,9 +484,10 @@ struct ExtdmHandle {
   }
 
   // ---------------------------------------------------------------- op shims
-  void conv(const View& out, const View& in0, const View* in1, const PackedW& w, int stride, int pad,
-            const float* bias, const View* res = nullptr, int act = ACT_NONE, const float* ps = nullptr,
-            const float* psh = nullptr, int per_channel = 0) {
+  // Returns the GroupNorm partial slots the conv wrote into `stats` (0: none).
+  int conv(const View& out, const View& in0, const View* in1, const PackedW& w, int stride, int pad,
+           const float* bias, const View* res = nullptr, int act = ACT_NONE, const float* ps = nullptr,
+           const float* psh = nullptr, int per_channel = 0, double* stats = nullptr, int stats_groups = 0) {
     REQUIRE((in1 ? in0.C + in1->C : in0.C) * w.KH * w.KW == w.K || w.mode == MODE_DECONV,
             "conv: input channels do not match the weight");
     REQUIRE(out.C == w.M, "conv: output channels do not match the weight");
@@ -492,15 +495,17 @@ struct ExtdmHandle {
             "conv: batch of an operand does not match the output");
     REQUIRE(w.mode != MODE_CONV || stride != 1 || (in0.T == out.T && (!in1 || in1->T == out.T)),
             "conv: frame count of an operand does not match the output");
-    if (plan) return;
+    if (plan) return 0;
     ConvEpi e;
     e.bias = bias;
+    e.stats = stats;
+    e.stats_groups = stats_groups;
     if (res) { e.res = res->p; e.res_sb = res->sb; e.res_sc = res->sc; e.res_st = res->st; }
     e.act = act;
     e.post_scale = ps;
     e.post_shift = psh;
     e.post_per_channel = per_channel;
-    conv_forward(s, out, in0, in1, w, stride, pad, e);
+    return conv_forward(s, out, in0, in1, w, stride, pad, e);
   }
 
   // ----------------------------------------------------------- Unet blocks
@@ -509,23 +514,27 @@ struct ExtdmHandle {
     Scope sc(arena);
     const int B = out.B, C = out.C, T = out.T, Hh = out.H, Ww = out.W;
     View h1 = alloc_cf(B, C, T, Hh, Ww);
-    conv(h1, in0, in1, P(p + ".block1.proj.weight"), 1, 1, D(p + ".block1.proj.bias"));
+    // the GroupNorm statistics of h1 / h2 come from the convs' epilogues where supported
+    double* st = fuse_gn_stats ? partials : nullptr;
+    const int sp1 = conv(h1, in0, in1, P(p + ".block1.proj.weight"), 1, 1, D(p + ".block1.proj.bias"), nullptr,
+                         ACT_NONE, nullptr, nullptr, 0, st, 8);
     const bool has_mlp = film_row.count(p) != 0;
     if (!plan)
       groupnorm_silu(s, h1, h1, 8, D(p + ".block1.norm.weight"), D(p + ".block1.norm.bias"),
-                     has_mlp ? film : nullptr, has_mlp ? film_row[p] : 0, film_nt, t_batch, nullptr, partials);
+                     has_mlp ? film : nullptr, has_mlp ? film_row[p] : 0, film_nt, t_batch, nullptr, partials, sp1);
     View h2 = alloc_cf(B, C, T, Hh, Ww);
-    conv(h2, h1, nullptr, P(p + ".block2.proj.weight"), 1, 1, D(p + ".block2.proj.bias"));
+    const int sp2 = conv(h2, h1, nullptr, P(p + ".block2.proj.weight"), 1, 1, D(p + ".block2.proj.bias"), nullptr,
+                         ACT_NONE, nullptr, nullptr, 0, st, 8);
     if (has(p + ".res_conv.weight")) {
       if (!plan)
         groupnorm_silu(s, h2, h2, 8, D(p + ".block2.norm.weight"), D(p + ".block2.norm.bias"), nullptr, 0, 0,
-                       nullptr, nullptr, partials);
+                       nullptr, nullptr, partials, sp2);
       conv(out, in0, in1, P(p + ".res_conv.weight"), 1, 0, D(p + ".res_conv.bias"), &h2);
     } else {
       REQUIRE(in1 == nullptr && in0.C == C, "identity residual needs matching channels");
       if (!plan)
         groupnorm_silu(s, h2, out, 8, D(p + ".block2.norm.weight"), D(p + ".block2.norm.bias"), nullptr, 0, 0,
-                       nullptr, &in0, partials);
+                       nullptr, &in0, partials, sp2);
     }
   }
 

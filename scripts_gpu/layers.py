@@ -20,6 +20,7 @@ for prec in precs:
     h = pkg._lib.Handle(ucfg, 1000, B, 0, precision=prec)
     h.load_state(sd)
     h.finalize()
+    h.bench_layer(B, layers[0], iters)  # clock ramp
     for layer in layers:
         ms, flops = h.bench_layer(B, layer, iters)
         print(f'{prec:6s} layer {layer} B={B}: {ms * 1e3:9.1f} us/launch, {flops / ms / 1e9:7.1f} TFLOP/s', flush=True)
