@@ -47,6 +47,8 @@ struct X3Args {
   int TH, NP, nrow_tiles, RS, XPOS;
   int out_bytes, res_bytes;  // extents of out / e.res (buffer descriptors of the epilogue)
   int stats_split;           // GroupNorm partial slots per (b, group) when e.stats is set
+  // XOP: pre-split input operand (X3Op, kernels.h) copied by LDS-DMA instead of staged
+  const _Float16* xop; long xop_cg, xop_hl;  // halves per channel group / per hi|lo half
   ConvEpi e;
 };
 
@@ -94,7 +96,12 @@ template <> struct XMaxX3<3, 512> { static constexpr int v = 800; };
 // KY: ky rows per A slot (stage). KY = KS makes a stage a whole channel block: one
 // barrier per channel block instead of KS, and the X prefetch has all KS*KS*NG MFMA
 // steps to land (the KS consecutive packed slices of a channel block are contiguous).
-template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS>
+// XOP: the input is a pre-split operand (X3Op: hi / lo fp16 in (hl, c8) planes of
+// zero-padded positions; written by groupnorm_silu_x3op): each channel block's halo tile
+// is one contiguous run per plane, copied by LDS-DMA into the second X buffer during the
+// block's first stage as [hl][c8][pos][8]: no staging registers, loads, conversions or
+// LDS stores, and a lane's k-slice is 16 consecutive bytes (no swizzle needed).
+template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false>
 __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   constexpr int NT = NW * 64;
   constexpr int PAD = KS / 2;
@@ -110,9 +117,14 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   constexpr int TM = BM / (32 * WM);
   constexpr int TN = BN / (32 * WN);
   static_assert(TM >= 1 && TN >= 1 && WM * WN == NW, "bad tile");
+  static_assert(!XOP || (NG == 1 && XBUF == 2 && SPAN), "operand input: one group, two X buffers");
 
   extern __shared__ __attribute__((aligned(16))) _Float16 smx[];
-  const int XH = a.XPOS * NG * 32;  // halves per X slot (hi + lo)
+  // halves from an X slot's hi block to its lo block (DMA mode: two c8 planes of whole
+  // 1 KiB pieces each)
+  const int XPL = ((a.XPOS + 63) & ~63) * 8;  // DMA mode: halves per (hl, c8) plane
+  const int XLO = XOP ? 2 * XPL : NG * a.XPOS * 16;
+  const int XH = 2 * XLO;  // halves per X slot (hi + lo)
   _Float16* As0 = smx;
   _Float16* As1 = smx + AHS;
   _Float16* Xs0 = smx + 2 * AHS;
@@ -126,6 +138,8 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   const int row0 = (tile % a.nrow_tiles) * a.TH;
   const int mtile = blockIdx.y;
   const int THK = a.TH + KS - 1;
+  // first halo position of the tile in the operand's padded [P][H+KS-1][RS] planes
+  const int tb = (plane0 * (a.H + KS - 1) + row0) * a.RS;
   const int NIT = a.ncgb * STG;
   const _Float16* wt = a.w + (long)mtile * a.ncgb * KS * AH;
 
@@ -255,7 +269,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
       const int sw = (spos[j] >> 3) & 1;
       const bool used = sg[j] >= 0;
       _Float16* dh = used ? Xs + ((long)sg[j] * a.XPOS + spos[j]) * 16 : xdummy;
-      _Float16* dl = used ? dh + (long)NG * a.XPOS * 16 : xdummy + 16;
+      _Float16* dl = used ? dh + XLO : xdummy + 16;
       *reinterpret_cast<h8*>(dh + 8 * sw) = hi0;
       *reinterpret_cast<h8*>(dh + 8 * (sw ^ 1)) = hi1;
       *reinterpret_cast<h8*>(dl + 8 * sw) = lo0;
@@ -271,6 +285,17 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
       else
         __builtin_amdgcn_global_load_lds((const void*)(src + pc * 512 + lane * 8), (lds_ptr_t)(As + pc * 512), 16, 0,
                                          0);
+    }
+  };
+
+  // operand input: the channel block's tile, four (hl, c8) runs of XPOS 16-B records
+  auto dma_x = [&](int cgb, _Float16* Xs) __attribute__((always_inline)) {
+    const _Float16* src = a.xop + (long)cgb * a.xop_cg + (long)tb * 8;
+    const int npc = (a.XPOS + 63) >> 6;  // 1 KiB pieces per plane
+    for (int pc = wave_u; pc < 4 * npc; pc += NW) {
+      const int pl = pc / npc, k = pc - pl * npc;  // pl = 2 * hl + c8
+      glds16_asm(src + (pl >> 1) * a.xop_hl + (pl & 1) * (a.xop_hl >> 1) + k * 512 + lane * 8,
+                 Xs + pl * XPL + k * 512);
     }
   };
 
@@ -302,9 +327,14 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
     ep_sc[tid] = a.wscale[mc];
     ep_bi[tid] = a.e.bias ? a.e.bias[mc] : 0.f;
   }
-  load_x(0);
-  load_a(0, As0);
-  store_x(Xs0, 0);
+  if (XOP) {
+    dma_x(0, Xs0);
+    load_a(0, As0);
+  } else {
+    load_x(0);
+    load_a(0, As0);
+    store_x(Xs0, 0);
+  }
   if (SPAN) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the asm DMA is invisible to __syncthreads
   else __syncthreads();
   // One (channel block, ky block) stage. `more` = a next channel block exists (its X is
@@ -320,7 +350,10 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
     if (it + 1 < NIT) load_a(it + 1, (it & 1) ? As0 : As1);
     const bool pre = (kb == 0) && more;
     if (SPAN) __builtin_amdgcn_sched_barrier(0);  // the X loads issue after the DMA (vmcnt order)
-    if (pre) load_x(cgb + 1);
+    if (pre) {
+      if (XOP) dma_x(cgb + 1, (cgb & 1) ? Xs0 : Xs1);
+      else load_x(cgb + 1);
+    }
 #pragma unroll
     for (int kyl = 0; kyl < KY; ++kyl) {
     const int ky = kb * KY + kyl;
@@ -340,9 +373,10 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int pos = bpos[j] + ky * a.RS + kx;
-          const _Float16* bp = Xs + ((long)g * a.XPOS + pos) * 16 + 8 * (h ^ ((pos >> 3) & 1));
+          const _Float16* bp = XOP ? Xs + h * XPL + pos * 8
+                                   : Xs + ((long)g * a.XPOS + pos) * 16 + 8 * (h ^ ((pos >> 3) & 1));
           bh[j] = *reinterpret_cast<const h8*>(bp);
-          bl[j] = *reinterpret_cast<const h8*>(bp + (long)NG * a.XPOS * 16);
+          bl[j] = *reinterpret_cast<const h8*>(bp + XLO);
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -355,7 +389,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
       }
     }
     }
-    if (kb == STG - 1 && more) {
+    if (!XOP && kb == STG - 1 && more) {
       if (XBUF == 1) {  // single X buffer: every wave is done with it
         if (SPAN) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else __syncthreads();
@@ -367,7 +401,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
       // writes; the prefetch loads (16 per slot) may stay in flight across the barrier
       // (only at ky = 0: a later stage's DMA is younger than the X loads, and vmcnt
       // retires in issue order, so waiting for it is vmcnt(0))
-      if (pre && STG > 1) {
+      if (!XOP && pre && STG > 1) {
         asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(16 * NSLOT) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -519,19 +553,20 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   }
 }
 
-template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS>
+template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false>
 void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
   constexpr int AH = KY * NG * KS * (BM / 32) * 2 * 512;
+  const size_t xlo = XOP ? (size_t)((a.XPOS + 63) & ~63) * 16 : (size_t)a.XPOS * NG * 16;
   // + 32 halves (unused-slot dummy) + 2 * BM floats (epilogue scale / bias)
-  const size_t lds = ((size_t)2 * AH + (size_t)XBUF * a.XPOS * NG * 32 + 32 + 4 * BM) * sizeof(_Float16);
+  const size_t lds = ((size_t)2 * AH + (size_t)XBUF * 2 * xlo + 32 + 4 * BM) * sizeof(_Float16);
   dim3 grid(ntiles, (a.Cout + BM - 1) / BM);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS>), grid, dim3(NW * 64), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP>), grid, dim3(NW * 64), lds, s, a);
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN>
@@ -549,6 +584,11 @@ void launch_ns(hipStream_t s, const X3Args& a, unsigned ntiles) {
     else if (need == 2) launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 2>(s, a, ntiles);
     else launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 3>(s, a, ntiles);
   }
+}
+
+int x3_v3() {
+  static const int v3 = [] { const char* v = getenv("EXTDM_X3_V3"); return v ? atoi(v) : 0; }();
+  return v3;
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF>
@@ -575,8 +615,11 @@ X3Tile x3_tile(int ks, int cout) {
   return t;
 }
 
-bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
-                     const ConvEpi& epi, int* stats_slots) {
+namespace {
+
+// Tile geometry, operands and epilogue of one conv_x3 launch; false if not covered.
+bool x3_setup(const View& out, const View& in0, const View* in1, const PackedW& w, const ConvEpi& epi, X3Args& a,
+              unsigned& ntiles, int* stats_slots) {
   if (stats_slots) *stats_slots = 0;
   if (!w.wx || w.mode != MODE_CONV) return false;
   const int ks = w.KH;
@@ -585,7 +628,7 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   if (out.H != H || out.W != W || W > tl.bn || tl.bn % W != 0) return false;
   // 32-bit in-plane offsets in the staging
   if ((long)in0.B * in0.sb > (1L << 31) || (in1 && (long)in1->B * in1->sb > (1L << 31))) return false;
-  X3Args a{};
+  a = X3Args{};
   a.TH = std::min(H, tl.bn / W);
   if (tl.bn % (a.TH * W) != 0) return false;
   a.NP = tl.bn / (a.TH * W);
@@ -610,6 +653,7 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   if (ob >= (1L << 31) - 4 || rb >= (1L << 31) - 4) return false;
   a.out_bytes = (int)ob;
   a.res_bytes = (int)rb;
+  ntiles = (unsigned)(((a.P + a.NP - 1) / a.NP) * a.nrow_tiles);
   // GroupNorm partials in the epilogue: whole tiles inside one sample, groups of whole
   // 8-row blocks inside one m-tile, at most 64 slots (the runtime's partials buffer)
   if (epi.stats) {
@@ -624,7 +668,18 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
       a.e.stats = nullptr;
     }
   }
-  const unsigned ntiles = (unsigned)(((a.P + a.NP - 1) / a.NP) * a.nrow_tiles);
+  return true;
+}
+
+}  // namespace
+
+bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
+                     const ConvEpi& epi, int* stats_slots) {
+  X3Args a;
+  unsigned ntiles = 0;
+  if (!x3_setup(out, in0, in1, w, epi, a, ntiles, stats_slots)) return false;
+  const int ks = w.KH;
+  const X3Tile tl{w.xbm, w.xbn, w.xng};
   if (tl.bn == 512) {
     if (ks == 7 && tl.bm == 64) launch<7, 1, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
     else if (ks == 3 && tl.bm == 64) launch<3, 1, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
@@ -637,14 +692,60 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     // workgroup per CU at 117 KB of LDS). Default: 4 waves of 64 x 64 (12 MFMAs per 8
     // ds_read_b128 instead of 6 per 6) at 68 KB, two independent workgroups per CU,
     // 12 % faster on the level-0 64 -> 64 conv at B = 64.
-    static const int v3 = [] { const char* v = getenv("EXTDM_X3_V3"); return v ? atoi(v) : 0; }();
-    if (v3 == 1) launch<3, 3, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
+    if (x3_v3() == 1) launch<3, 3, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
     else launch<3, 1, 64, 256, 1, 4, 4, 2>(s, a, ntiles);
   }
   else if (ks == 3 && tl.bm == 128) launch<3, 1, 128, 128, 1, 2, 8, 2>(s, a, ntiles);
   else if (ks == 1 && tl.bm == 64) launch<1, 1, 64, 128, 2, 4, 4, 2>(s, a, ntiles);
   else if (ks == 1 && tl.bm == 128) launch<1, 1, 128, 128, 2, 2, 4, 2>(s, a, ntiles);
   else return false;
+  return true;
+}
+
+size_t x3op_halves(int B, int C, int T, int H, int W, int pad) {
+  // + one plane and 1 KiB of slack: the last tile's DMA pieces read past the last position
+  const size_t plane = (size_t)(H + 2 * pad) * (W + 2 * pad) * 16;
+  return 2 * (size_t)(C / 16) * B * T * plane + plane + 512;
+}
+
+bool conv_x3_op_supported(const View& out, const PackedW& w, int C, int pad) {
+  if (!w.wx || w.mode != MODE_CONV || w.KH != 3 || w.KW != 3 || pad != 1 || w.xng != 1 || C % 16 != 0) return false;
+  // EXTDM_NO_X3OP=1: the producer writes fp32 and the conv stages it (A/B)
+  static const bool off = [] {
+    auto on = [](const char* n) { const char* v = getenv(n); return v && v[0] && v[0] != '0'; };
+    return on("EXTDM_X3_NOSPAN") || on("EXTDM_NO_X3OP");
+  }();
+  if (off) return false;
+  const int H = out.H, W = out.W, bn = w.xbn;
+  if (W > bn || bn % W != 0) return false;
+  const int TH = std::min(H, bn / W);
+  if (bn % (TH * W) != 0 || H % TH != 0) return false;
+  const int NP = bn / (TH * W);
+  if ((out.B * out.T) % NP != 0) return false;
+  return w.xbm == 64 ? bn == 256 : (w.xbm == 128 && bn == 128);
+}
+
+bool conv_x3_forward_op(hipStream_t s, const View& out, const X3Op& in, const PackedW& w, const ConvEpi& epi,
+                        int* stats_slots) {
+  if (stats_slots) *stats_slots = 0;
+  if (!conv_x3_op_supported(out, w, in.C, in.pad) || in.H != out.H || in.W != out.W || in.B != out.B ||
+      in.T != out.T)
+    return false;
+  // geometry from a channel-first stand-in of the operand's activation (no staging reads)
+  const View g = cf_view(nullptr, in.B, in.C, in.T, in.H, in.W);
+  X3Args a;
+  unsigned ntiles = 0;
+  if (!x3_setup(out, g, nullptr, w, epi, a, ntiles, stats_slots)) return false;
+  const size_t plane = (size_t)(in.H + 2 * in.pad) * (in.W + 2 * in.pad) * 8;  // one (hl, c8) plane
+  a.xop = in.p;
+  a.xop_cg = (long)((size_t)in.B * in.T * plane);
+  a.xop_hl = 2 * (long)((size_t)(in.C / 16) * in.B * in.T * plane);
+  if (w.xbm == 64) {
+    if (x3_v3() == 1) launch_sp<3, 3, 64, 256, 1, 4, 8, 2, true, 1, true>(s, a, ntiles);
+    else launch_sp<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true>(s, a, ntiles);
+  } else {
+    launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true>(s, a, ntiles);
+  }
   return true;
 }
 

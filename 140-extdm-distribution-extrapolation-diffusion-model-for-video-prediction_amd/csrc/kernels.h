@@ -97,6 +97,19 @@ X3Tile x3_tile(int ks, int cout);
 // the epilogue wrote (0: not computed, the caller runs the statistics pass).
 bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                      const ConvEpi& epi, int* stats_slots = nullptr);
+// Pre-split f16x3 conv input ("operand") of an activation [B][C][T][H][W]: hi / lo fp16
+// halves as [hl][c8][C/16][B*T][H+2*pad][W+2*pad][8] with a zero ring of width pad:
+// channel 16*cg + 8*c8 + e of a padded position is element e of its 16-B record in
+// plane (hl, c8) — the MFMA k-slice a lane of half c8 reads, one ds_read_b128 each.
+struct X3Op {
+  _Float16* p = nullptr;
+  int B = 0, C = 0, T = 0, H = 0, W = 0, pad = 0;
+};
+size_t x3op_halves(int B, int C, int T, int H, int W, int pad);  // allocation incl. DMA slack
+// Whether conv_x3_forward_op covers this conv (3x3 'same', C % 16 == 0, whole tiles).
+bool conv_x3_op_supported(const View& out, const PackedW& w, int C, int pad);
+bool conv_x3_forward_op(hipStream_t s, const View& out, const X3Op& in, const PackedW& w, const ConvEpi& epi,
+                        int* stats_slots = nullptr);
 void x3_range_reset(hipStream_t s);
 int* x3_range_ptr();  // device address of the flag on the current device
 int x3_range_read(hipStream_t s);
@@ -113,6 +126,11 @@ void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, c
                     const View* res, double* partials, int given_split = 0);
 // given_split > 0: `partials` already holds that many (sum, sumsq) slots per (b, group)
 // (written by the producing conv's epilogue); the statistics pass is skipped.
+// The same GroupNorm + FiLM + SiLU written as the pre-split operand of the next 3x3 conv
+// (its only consumer), instead of fp32.
+void groupnorm_silu_x3op(hipStream_t s, const View& x, const X3Op& out, int groups, const float* gamma,
+                         const float* beta, const float* film, int film_row, int film_nt, const int* t_batch,
+                         double* partials, int given_split = 0);
 
 // Channel LayerNorm (biased var over C, gamma only; u12:138-147) of in0 ++ in1.
 void channel_ln(hipStream_t s, const View& out, const View& in0, const View* in1, const float* gamma);

@@ -519,12 +519,33 @@ struct ExtdmHandle {
     const int sp1 = conv(h1, in0, in1, P(p + ".block1.proj.weight"), 1, 1, D(p + ".block1.proj.bias"), nullptr,
                          ACT_NONE, nullptr, nullptr, 0, st, 8);
     const bool has_mlp = film_row.count(p) != 0;
-    if (!plan)
-      groupnorm_silu(s, h1, h1, 8, D(p + ".block1.norm.weight"), D(p + ".block1.norm.bias"),
-                     has_mlp ? film : nullptr, has_mlp ? film_row[p] : 0, film_nt, t_batch, nullptr, partials, sp1);
-    View h2 = alloc_cf(B, C, T, Hh, Ww);
-    const int sp2 = conv(h2, h1, nullptr, P(p + ".block2.proj.weight"), 1, 1, D(p + ".block2.proj.bias"), nullptr,
-                         ACT_NONE, nullptr, nullptr, 0, st, 8);
+    const PackedW& w2 = P(p + ".block2.proj.weight");
+    int sp2 = 0;
+    View h2;
+    if (cfg.precision == EXTDM_PRECISION_F16X3 && conv_x3_op_supported(cf_view(nullptr, B, C, T, Hh, Ww), w2, C, 1)) {
+      // block1's GroupNorm + FiLM + SiLU is written straight as block2's pre-split conv
+      // operand (hi / lo fp16, zero ring): the conv copies it by LDS-DMA, no staging
+      X3Op op;
+      op.B = B; op.C = C; op.T = T; op.H = Hh; op.W = Ww; op.pad = 1;
+      op.p = reinterpret_cast<_Float16*>(arena.alloc((x3op_halves(B, C, T, Hh, Ww, 1) + 1) / 2));
+      if (!plan)
+        groupnorm_silu_x3op(s, h1, op, 8, D(p + ".block1.norm.weight"), D(p + ".block1.norm.bias"),
+                            has_mlp ? film : nullptr, has_mlp ? film_row[p] : 0, film_nt, t_batch, partials, sp1);
+      h2 = alloc_cf(B, C, T, Hh, Ww);
+      if (!plan) {
+        ConvEpi e;
+        e.bias = D(p + ".block2.proj.bias");
+        e.stats = st;
+        e.stats_groups = 8;
+        REQUIRE(conv_x3_forward_op(s, h2, op, w2, e, &sp2), "block2 conv: operand input not covered");
+      }
+    } else {
+      if (!plan)
+        groupnorm_silu(s, h1, h1, 8, D(p + ".block1.norm.weight"), D(p + ".block1.norm.bias"),
+                       has_mlp ? film : nullptr, has_mlp ? film_row[p] : 0, film_nt, t_batch, nullptr, partials, sp1);
+      h2 = alloc_cf(B, C, T, Hh, Ww);
+      sp2 = conv(h2, h1, nullptr, w2, 1, 1, D(p + ".block2.proj.bias"), nullptr, ACT_NONE, nullptr, nullptr, 0, st, 8);
+    }
     if (has(p + ".res_conv.weight")) {
       if (!plan)
         groupnorm_silu(s, h2, h2, 8, D(p + ".block2.norm.weight"), D(p + ".block2.norm.bias"), nullptr, 0, 0,
@@ -1531,7 +1552,8 @@ struct ExtdmHandle {
     arena.top = 0;
     const size_t n = (size_t)3 * cfg.tp * cfg.latent * cfg.latent;
     eps_buf = dmalloc((size_t)B * n * sizeof(float));
-    partials = reinterpret_cast<double*>(dmalloc((size_t)B * 8 * 64 * 2 * sizeof(double)));
+    // GroupNorm: [B][8 groups][64 slots][sum, sumsq], then (mean, rstd) per (b, group)
+    partials = reinterpret_cast<double*>(dmalloc(((size_t)B * 8 * 64 * 2 + (size_t)B * 8) * sizeof(double)));
     t_batch = reinterpret_cast<int*>(dmalloc((size_t)std::max(B, 1) * sizeof(int)));
     step_ctr = reinterpret_cast<int*>(dmalloc(sizeof(int) * 4));
     HIPCHK(hipStreamCreateWithFlags(&work, hipStreamNonBlocking));
