@@ -1817,11 +1817,14 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     const int T = h->frames(), L = h->cfg.latent;
     // layer 0: init_conv, conv3d (1,7,7) channels -> dim over (B, T, L, L) (u12:913, 1041),
     // input as the forward issues it: two sources (x-branch, cond_fea branch).
-    // layers 1-4: ResnetBlock convs (u12:165, 200) at levels 0-2 and a level-0 res_conv.
+    // layers 1-4: ResnetBlock convs (u12:165, 200) at levels 0-2 and a level-0 res_conv,
+    // fp32 input staged by the conv; layer 5: the level-0 block2 conv as the forward issues
+    // it, from block1's pre-split operand (groupnorm_silu_x3op, written once untimed).
     static const char* names[] = {"init_conv.weight", "downs.0.0.block2.proj.weight", "downs.1.0.block2.proj.weight",
-                                  "downs.2.0.block2.proj.weight", "ups.3.0.res_conv.weight"};
-    static const int levels[] = {0, 0, 1, 2, 0};
-    REQUIRE(layer >= 0 && layer < 5, "unknown layer id");
+                                  "downs.2.0.block2.proj.weight", "ups.3.0.res_conv.weight",
+                                  "downs.0.0.block2.proj.weight"};
+    static const int levels[] = {0, 0, 1, 2, 0, 0};
+    REQUIRE(layer >= 0 && layer < 6, "unknown layer id");
     std::string wn = names[layer];
     // with the composed x-branch (xpath_x3.hip) the forward's init_conv launch is the
     // cond_fea branch alone: 256 -> 64 channels (init_conv.weight[:, 256:])
@@ -1845,12 +1848,30 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     const std::string bn = wn.substr(0, wn.size() - 6) + "bias";
     float* bias = h->has(bn) ? h->D(bn) : nullptr;
     const View* in1 = c1 ? &fup : nullptr;
-    h->conv(r, x0, in1, w, 1, ks / 2, bias);  // warm
+    X3Op op;
+    if (layer == 5) {
+      REQUIRE(h->cfg.precision == EXTDM_PRECISION_F16X3 && conv_x3_op_supported(r, w, c0, 1),
+              "bench layer 5: the operand-input conv is not covered (f16x3 only)");
+      op.B = B; op.C = c0; op.T = T; op.H = Lq; op.W = Lq; op.pad = 1;
+      op.p = reinterpret_cast<_Float16*>(h->arena.alloc((x3op_halves(B, c0, T, Lq, Lq, 1) + 1) / 2));
+      groupnorm_silu_x3op(s, x0, op, 8, h->D("downs.0.0.block1.norm.weight"), h->D("downs.0.0.block1.norm.bias"),
+                          nullptr, 0, 0, nullptr, h->partials, 0);
+    }
+    auto launch = [&] {
+      if (layer == 5) {
+        ConvEpi e;
+        e.bias = bias;
+        REQUIRE(conv_x3_forward_op(s, r, op, w, e), "bench layer 5: launch not covered");
+      } else {
+        h->conv(r, x0, in1, w, 1, ks / 2, bias);
+      }
+    };
+    launch();  // warm
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     HIPCHK(hipEventRecord(a, s));
-    for (int i = 0; i < iters; ++i) h->conv(r, x0, in1, w, 1, ks / 2, bias);
+    for (int i = 0; i < iters; ++i) launch();
     HIPCHK(hipEventRecord(b, s));
     HIPCHK(hipEventSynchronize(b));
     float ms = 0.f;

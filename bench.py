@@ -54,6 +54,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 matrix peak
 # f16x3: three v_mfma_f32_32x32x16_f16 per fp32 product; fp16 dense MFMA peak 2516.6 TF/s
 # (32x32x16 = 32768 FLOP per 32 cycles per SIMD, 1024 SIMDs, 2.4 GHz) / 3
 F16X3_PEAK_TFLOPS = 2516.6 / 3
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak
 
 
 def parse(argv=None):
@@ -180,11 +181,15 @@ class NativeWorkload:
 
     # extdm_bench_layer ids (runtime.cpp) of the kernels reported, dominant first: the
     # level-0 ResnetBlock 3x3 conv (64 -> 64 at 32x32, the largest share of GPU time per
-    # step, profiles/r02_*_kernel_stats.csv), init_conv's cond_fea branch (256 -> 64, 7x7;
-    # the x-branch is the composed xpath_x3 kernel) and the level-0 1x1 res_conv (128 -> 64)
-    LAYERS = [(1, 'conv_x3_kernel<3,64,256,1,4,8,2>', 'level-0 ResnetBlock conv 64->64 1x3x3'),
-              (0, 'conv_x3_kernel<7,64,512,1,8,16,1>', 'init_conv cond_fea branch 256->64 1x7x7'),
-              (4, 'conv_x3_kernel<1,64,128,2,4,4,2>', 'level-0 res_conv 128->64 1x1x1')]
+    # step, profiles/r02_*_kernel_stats.csv; block1's conv stages an fp32 input, block2's
+    # copies block1's pre-split operand, id 5), init_conv's cond_fea branch (256 -> 64,
+    # 7x7; the x-branch is the composed xpath_x3 kernel) and the level-0 1x1 res_conv
+    # (128 -> 64), which is HBM-bound: 3 FLOP-equivalents of f16x3 MFMA per 4-B element
+    # moved is far below the machine balance, so it is priced against HBM bytes.
+    LAYERS = [(1, 'mfma', 'conv_x3_kernel<3,1,64,256,1,4,4,2,SPAN,NS=2>', 'level-0 ResnetBlock block1 conv 64->64 1x3x3, fp32 input staged', 64, 64),
+              (5, 'mfma', 'conv_x3_kernel<3,1,64,256,1,4,4,2,SPAN,XOP>', 'level-0 ResnetBlock block2 conv 64->64 1x3x3, pre-split operand by LDS-DMA', 64, 64),
+              (0, 'mfma', 'conv_x3_kernel<7,1,64,512,1,8,16,1>', 'init_conv cond_fea branch 256->64 1x7x7', 256, 64),
+              (4, 'hbm', 'conv_x3_kernel<1,1,64,128,2,4,4,2>', 'level-0 res_conv 128->64 1x1x1', 128, 64)]
 
     def _traffic(self, layer):
         """HBM bytes per launch from the committed PMC passes (scripts_gpu/pmc_layers.sh)."""
@@ -198,19 +203,33 @@ class NativeWorkload:
         return None
 
     def roofline(self):
-        """Per kernel: FLOP per launch / average launch time over 20 launches of the exact
-        forward launch, timed with HIP events on the handle's stream (extdm_bench_layer).
-        The first entry is the dominant kernel; the others ride along under `others`."""
+        """Per kernel, timed over 20 launches of the exact forward launch with HIP events
+        on the handle's stream (extdm_bench_layer). MFMA-bound: FLOP per launch / time
+        against the f16x3 peak (dense fp16 MFMA / 3). HBM-bound: algorithmic bytes per
+        launch (fp32 input + output elements, 4 B each, weights aside) / time against
+        8 TB/s. The first entry is the dominant kernel; the others ride along."""
         B = self.args.batch
         peak = F16X3_PEAK_TFLOPS if self.precision == 'f16x3' else FP32_MFMA_PEAK_TFLOPS
+        u = self.fd.unet.ucfg
+        T = self.tc + self.tp
         out = []
-        for layer, kname, what in self.LAYERS:
+        for layer, bound, kname, what, cin, cout in self.LAYERS:
+            if layer == 5 and self.precision != 'f16x3':
+                continue
             ms_layer, flops = self.h.bench_layer(B, layer, 20)
-            achieved = flops / (ms_layer * 1e-3) / 1e12
-            out.append({'bound': 'mfma', 'kernel': f'{kname} ({what}, {self.precision})',
-                        'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
-                        'frac': round(achieved / peak, 4), 'traffic': self._traffic(layer),
-                        'launch_ms': round(ms_layer, 4), 'flop_per_launch': flops})
+            traffic = self._traffic(layer)
+            if bound == 'mfma':
+                achieved = flops / (ms_layer * 1e-3) / 1e12
+                e = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
+                     'frac': round(achieved / peak, 4), 'flop_per_launch': flops}
+            else:
+                nbytes = 4 * B * T * u.latent * u.latent * (cin + cout)
+                achieved = nbytes / (ms_layer * 1e-3) / 1e9
+                e = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'bytes_per_launch': nbytes}
+            e.update({'kernel': f'{kname} ({what}, {self.precision})', 'traffic': traffic,
+                      'launch_ms': round(ms_layer, 4)})
+            out.append(e)
         res = out[0]
         res['others'] = out[1:]
         return res

@@ -112,8 +112,9 @@ int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, fl
  * exactly as the forward issues it, on random operands, with HIP events on the
  * handle's stream; returns the average ms per launch and the algorithmic FLOPs
  * per launch. layer 0 = init_conv (1,7,7) channels->dim (two sources); 1, 2, 3 =
- * ResnetBlock (1,3,3) convs at levels 0, 1, 2 (downs.{0,1,2}.0.block2); 4 = the
- * level-0 up ResnetBlock's 1x1 res_conv (ups.3.0.res_conv). */
+ * ResnetBlock (1,3,3) convs at levels 0, 1, 2 (downs.{0,1,2}.0.block2) from an fp32
+ * input; 4 = the level-0 up ResnetBlock's 1x1 res_conv (ups.3.0.res_conv); 5 = the
+ * level-0 block2 conv from block1's pre-split operand, as the F16X3 forward issues it. */
 int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out, double* flops_out);
 
 /* The F16X3 activation-range flag: nonzero if an operand split since the last reset

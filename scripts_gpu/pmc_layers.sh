@@ -4,7 +4,7 @@
 # summarised with the gfx950 FETCH_SIZE x2 correction (scripts_gpu/pmc_summary.py).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 B=${B:-64}
-for spec in "1:conv_x3_kernel<3, 64, 256" "0:conv_x3_kernel<7, 64, 512" "4:conv_x3_kernel<1, 64, 128"; do
+for spec in "1:conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false>" "5:conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true>" "0:conv_x3_kernel<7, 1, 64, 512, 1, 8, 16, 1, true, 1, false>" "4:conv_x3_kernel<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false>"; do
   L=${spec%%:*}; PAT=${spec#*:}
   for C in FETCH_SIZE WRITE_SIZE; do
     rm -rf gpurun_out/pmc_${L}_$C
