@@ -12,7 +12,7 @@ EXPORTS = ['extdm_create', 'extdm_destroy', 'extdm_last_error', 'extdm_load_weig
            'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_bench_layer',
            'extdm_decode', 'extdm_set_lfae', 'extdm_region_params', 'extdm_region_hw', 'extdm_bg_params',
            'extdm_flow_predict', 'extdm_flow_hw', 'extdm_bottleneck', 'extdm_range_flag',
-           'extdm_attn_layer']
+           'extdm_attn_layer', 'extdm_frame_metrics_workspace', 'extdm_frame_metrics']
 
 BG_TYPES = {'zero': 0, 'shift': 1, 'affine': 2, 'perspective': 3}
 
@@ -97,6 +97,11 @@ def load():
     L.extdm_attn_layer.restype = i32
     L.extdm_range_flag.argtypes = [vp, i32, vp]
     L.extdm_range_flag.restype = i32
+    L.extdm_frame_metrics_workspace.argtypes = [i32, i32, i32, i32, i32]
+    L.extdm_frame_metrics_workspace.restype = ctypes.c_size_t
+    L.extdm_frame_metrics.argtypes = [vp, vp, i32, i32, i32, i32, i32, ctypes.c_long, ctypes.c_long, ctypes.c_long,
+                                      vp, vp, vp, vp]
+    L.extdm_frame_metrics.restype = i32
     _lib = L
     return L
 

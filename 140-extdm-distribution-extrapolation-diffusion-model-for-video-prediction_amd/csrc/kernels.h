@@ -111,6 +111,10 @@ bool conv_x3_op_supported(const View& out, const PackedW& w, int C, int pad);
 bool conv_x3_forward_op(hipStream_t s, const View& out, const X3Op& in, const PackedW& w, const ConvEpi& epi,
                         int* stats_slots = nullptr);
 void x3_range_reset(hipStream_t s);
+// Evaluation metrics (metrics.hip): per-frame PSNR and SSIM in fp64.
+size_t frame_metrics_workspace(int nframes, int C, int H);
+void frame_metrics(hipStream_t s, const float* a, const float* b, int N, int T, int C, int H, int W, long sN, long sT,
+                   long sC, double* psnr, double* ssim, double* work);
 int* x3_range_ptr();  // device address of the flag on the current device
 int x3_range_read(hipStream_t s);
 

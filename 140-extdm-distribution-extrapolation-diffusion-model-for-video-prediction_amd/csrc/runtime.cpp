@@ -1630,6 +1630,21 @@ extern "C" {
 
 const char* extdm_last_error(void) { return g_last_error.c_str(); }
 
+size_t extdm_frame_metrics_workspace(int N, int T, int C, int H, int W) {
+  (void)W;
+  return N > 0 && T > 0 && C > 0 && H > 10 ? frame_metrics_workspace(N * T, C, H) : 0;
+}
+
+int extdm_frame_metrics(const float* a, const float* b, int N, int T, int C, int H, int W, long sN, long sT, long sC,
+                        double* psnr, double* ssim, void* work, void* stream) {
+  return guarded([&] {
+    REQUIRE(a && b && psnr && ssim && work, "frame_metrics: null pointer");
+    frame_metrics(reinterpret_cast<hipStream_t>(stream), a, b, N, T, C, H, W, sN, sT, sC, psnr, ssim,
+                  reinterpret_cast<double*>(work));
+    HIPCHK(hipGetLastError());
+  });
+}
+
 int extdm_create(const ExtdmConfig* cfg, ExtdmHandle** out) {
   return guarded([&] {
     REQUIRE(cfg && out, "null argument");

@@ -27,10 +27,15 @@
  *   extdm_bg_params      BGMotionPredictor.forward     LFAE/bg_motion_predictor.py:47-64
  *   extdm_flow_predict   PixelwiseFlowPredictor.forward LFAE/pixelwise_flow_predictor.py:106-153
  *   extdm_bottleneck     Generator.forward_bottle      LFAE/generator.py:95-102
+ *   extdm_frame_metrics  img_psnr / calculate_ssim_function per frame (the per-frame
+ *                        loops of calculate_psnr2 / calculate_ssim2, valid.py:226-233)
+ *                                                   metrics/calculate_psnr.py:6-15,
+ *                                                   metrics/calculate_ssim.py:6-41
  */
 #ifndef EXTDM_H
 #define EXTDM_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -178,6 +183,15 @@ int extdm_flow_hw(const ExtdmHandle* h);
 /* Generator.forward_bottle / compute_fea (LFAE/generator.py:95-102, 202-206):
  * out [N][C_bottleneck][S / 2^d][S / 2^d]. */
 int extdm_bottleneck(ExtdmHandle* h, int N, const float* img, float* out, void* stream);
+
+/* Per-frame PSNR and SSIM of two frame sets a, b (device fp32, [N][T][C][H][W] through
+ * element strides sN, sT, sC; planes contiguous H*W) into device doubles psnr[N*T],
+ * ssim[N*T], in fp64 like the reference's numpy evaluation. C must be 1 or 3 and
+ * H, W > 10 (the 11x11 window's valid region). `work` is device scratch of
+ * extdm_frame_metrics_workspace() bytes. Not tied to a handle. */
+size_t extdm_frame_metrics_workspace(int N, int T, int C, int H, int W);
+int extdm_frame_metrics(const float* a, const float* b, int N, int T, int C, int H, int W, long sN, long sT, long sC,
+                        double* psnr, double* ssim, void* work, void* stream);
 
 #ifdef __cplusplus
 }

@@ -4,7 +4,8 @@ itself (read-only at /root/reference) on CPU in the build container.
 Only data leaves this script: inputs are regenerated from seeds at test time,
 outputs/checksums are stored as .npz/.json. Missing third-party packages are
 replaced by the stand-ins under tests/golden/shims/ (einops_exts, timm,
-skimage: import-only; rotary_embedding_torch: restatement of 0.8.3).
+skimage: import-only; rotary_embedding_torch: restatement of 0.8.3; cv2: the two
+OpenCV calls of calculate_ssim.py restated).
 
 Usage (build container only):  python tests/golden/make_golden.py
 """
@@ -319,7 +320,38 @@ def main():
     print('done')
 
 
+def metrics():
+    """The reference's own metric code (metrics/calculate_psnr.py, calculate_ssim.py with
+    the cv2 stand-in of shims/cv2, fvd.py frechet_distance) on seeded videos / features."""
+    from tests.golden_inputs import METRIC_CASES, metric_videos, metric_feats
+    from metrics.calculate_psnr import img_psnr, calculate_psnr, calculate_psnr2
+    from metrics.calculate_ssim import calculate_ssim_function, calculate_ssim, calculate_ssim2
+    from metrics.fvd import frechet_distance
+    out = {}
+    for name in METRIC_CASES:
+        a, b = metric_videos(name)
+        n, t = a.shape[:2]
+        out[f'{name}_psnr'] = np.array([[img_psnr(a[i, j].numpy(), b[i, j].numpy()) for j in range(t)]
+                                        for i in range(n)], dtype=np.float64)
+        out[f'{name}_ssim'] = np.array([[calculate_ssim_function(a[i, j].numpy(), b[i, j].numpy()) for j in range(t)]
+                                        for i in range(n)], dtype=np.float64)
+        out[f'{name}_psnr2'] = np.float64(calculate_psnr2(a, b))
+        out[f'{name}_ssim2'] = np.float64(calculate_ssim2(a, b))
+        out[f'{name}_psnr_avg'] = np.array(list(calculate_psnr(a, b)['psnr'].values()), dtype=np.float64)
+        out[f'{name}_ssim_std'] = np.array(list(calculate_ssim(a, b)['ssim_std'].values()), dtype=np.float64)
+    fake, real = metric_feats()
+    out['fd'] = np.float64(frechet_distance(fake, real))
+    out['fd_single'] = np.float64(frechet_distance(fake[:1], real))
+    out['fd_self'] = np.float64(frechet_distance(real, real))
+    np.savez_compressed(os.path.join(HERE, 'metrics.npz'), **out)
+    print('metrics done')
+
+
 if __name__ == '__main__':
+    if '--metrics' in sys.argv:
+        import_reference()
+        metrics()
+        sys.exit(0)
     if '--variants' in sys.argv or '--lfae' in sys.argv or '--wrappers' in sys.argv:
         torch.set_num_threads(8)
         import_reference()
@@ -334,3 +366,4 @@ if __name__ == '__main__':
         variants()
         lfae()
         wrappers()
+        metrics()

@@ -158,3 +158,25 @@ def lfae_config_dict(lc, ucfg, occ):
         'diffusion_params': {'model_params': {'null_cond_prob': 0.0, 'use_residual_flow': False,
                                               'only_use_flow': False, 'sampling_timesteps': 10, 'loss_type': 'l2'}},
     }
+
+
+# evaluation metrics (metrics.py; valid.py:199-243): seeded videos in [0, 1] as
+# [n, t, c, h, w] and I3D-sized (400-d) synthetic features
+METRIC_CASES = {'rgb': (3, 4, 3, 32, 32, 31), 'gray': (2, 3, 1, 24, 20, 32), 'rgb_wide': (2, 2, 3, 16, 40, 33)}
+
+
+def metric_videos(name):
+    n, t, c, h, w, seed = METRIC_CASES[name]
+    g = np.random.Generator(np.random.PCG64(seed))
+    a = g.random((n, t, c, h, w), dtype=np.float32)
+    noise = g.standard_normal((n, t, c, h, w)).astype(np.float32) * np.float32(0.05 * (1 + np.arange(n)[:, None, None, None, None]))
+    b = np.clip(a + noise, 0, 1).astype(np.float32)
+    b[0, 0] = a[0, 0]  # one identical frame: mse < 1e-10 -> 100 dB
+    return torch.from_numpy(a), torch.from_numpy(b)
+
+
+def metric_feats(seed=34):
+    g = np.random.Generator(np.random.PCG64(seed))
+    real = g.standard_normal((16, 400)).astype(np.float32)
+    fake = (g.standard_normal((12, 400)) * 1.2 + 0.3).astype(np.float32)
+    return fake, real
