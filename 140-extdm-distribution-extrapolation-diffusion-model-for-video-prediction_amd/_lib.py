@@ -20,7 +20,7 @@ SAMPLER_DDPM = 0
 SAMPLER_DDIM = 1
 
 # include/extdm.h EXTDM_PRECISION_*: arithmetic of the direct convolutions
-PRECISIONS = {'fp32': 0, 'f16x3': 1}
+PRECISIONS = {'fp32': 0, 'f16x3': 1, 'bf16_attn': 2}
 DEFAULT_PRECISION = os.environ.get('EXTDM_PRECISION', 'f16x3')
 
 class ExtdmConfig(ctypes.Structure):

@@ -150,6 +150,12 @@ struct AttnGeom {
   int ss0, ss1, ss2; // effective shift
   int Dp, Hp, Wp;    // padded extents
 };
+// bf16-MFMA attention core (attn_bf16.hip, EXTDM_PRECISION_BF16_ATTN): same operands and
+// geometry as window_attention, groups of <= 64 tokens (temporal: <= 32 frames), dim_head 32;
+// false if the shape is not covered. bias_dense [heads][bstride][bstride].
+bool attention_bf16(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads, int dim_head,
+                    const float* bias_dense, int bstride, const float* rope_cos, const float* rope_sin,
+                    float q_scale);
 // Unfused attention (dim_head 32, <= 32 tokens per group; e.g. C = 512 levels).
 // qkv: channel-first [B][3*heads*32][T][H][W]; o: [B][heads*32][T][H][W].
 void window_attention(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads,

@@ -158,10 +158,10 @@ struct ExtdmHandle {
     pw.w = dmalloc(a.size() * sizeof(float));
     HIPCHK(hipMemcpy(pw.w, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
     if (kh == kw && (kh == 1 || kh == 3 || kh == 7) && co > 32) pack_halo(pw, t.f, ci);
-    if (cfg.precision == EXTDM_PRECISION_F16X3 && kh == kw && (kh == 1 || kh == 3 || kh == 7) && co > 32 &&
+    if (x3_convs() && kh == kw && (kh == 1 || kh == 3 || kh == 7) && co > 32 &&
         ci >= 16)
       pack_x3(pw, t.f, ci);
-    if (cfg.precision == EXTDM_PRECISION_F16X3) pack_gemm_x3(pw, a, 1);
+    if (x3_convs()) pack_gemm_x3(pw, a, 1);
     return packed[n] = pw;
   }
   // f16x3 implicit-GEMM layout (conv_gemm_x3.hip) from the fp32 GEMM packing a
@@ -321,7 +321,7 @@ struct ExtdmHandle {
     }
     pw.w = dmalloc(a.size() * sizeof(float));
     HIPCHK(hipMemcpy(pw.w, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
-    if (cfg.precision == EXTDM_PRECISION_F16X3) pack_gemm_x3(pw, a, 4);
+    if (x3_convs()) pack_gemm_x3(pw, a, 4);
     return packed[n] = pw;
   }
   PackedW pack_matrix(const std::vector<float>& wrow /*[M][K]*/, int M, int K) {
@@ -347,7 +347,7 @@ struct ExtdmHandle {
   bool xpath_ready = false;
   bool xpath_enabled() const {
     static const bool off = [] { const char* v = getenv("EXTDM_NO_XPATH"); return v && v[0] && v[0] != '0'; }();
-    return !off && cfg.precision == EXTDM_PRECISION_F16X3 &&
+    return !off && x3_convs() &&
            (cfg.arch == EXTDM_ARCH_U12 || cfg.arch == EXTDM_ARCH_ADA) && cfg.latent >= 7 && cfg.dim <= 64;
   }
   const XPathW& Pxpath() {
@@ -522,7 +522,7 @@ struct ExtdmHandle {
     const PackedW& w2 = P(p + ".block2.proj.weight");
     int sp2 = 0;
     View h2;
-    if (cfg.precision == EXTDM_PRECISION_F16X3 && conv_x3_op_supported(cf_view(nullptr, B, C, T, Hh, Ww), w2, C, 1)) {
+    if (x3_convs() && conv_x3_op_supported(cf_view(nullptr, B, C, T, Hh, Ww), w2, C, 1)) {
       // block1's GroupNorm + FiLM + SiLU is written straight as block2's pre-split conv
       // operand (hi / lo fp16, zero ring): the conv copies it by LDS-DMA, no staging
       X3Op op;
@@ -668,6 +668,9 @@ struct ExtdmHandle {
     HIPCHK(hipMemcpy(r.sc, inv, 4 * sizeof(float), hipMemcpyHostToDevice));
     return attn_x3w[nqkv] = r;
   }
+  // f16x3 convolutions (F16X3, and BF16_ATTN, whose attention core alone is bf16)
+  bool x3_convs() const { return cfg.precision == EXTDM_PRECISION_F16X3 || cfg.precision == EXTDM_PRECISION_BF16_ATTN; }
+  bool bf16_attn() const { return cfg.precision == EXTDM_PRECISION_BF16_ATTN; }
   bool x3_attn_ok(int C, int ntok, int mode) const {
     auto flag = [](const char* n) { const char* v = getenv(n); return v && v[0] && v[0] != '0'; };
     // read per call: EXTDM_NO_X3_ATTN / _STW / _TEMPORAL route a layer back to the fp32 kernels
@@ -691,6 +694,22 @@ struct ExtdmHandle {
     // dense bias tables are laid out for the configured window (build_tables); a
     // collapsed window reads their leading N x N block (index[:N, :N], u12:476)
     const int bstride = cfg.window[0] * cfg.window[1] * cfg.window[2] <= 32 ? 32 : 64;
+    if (bf16_attn() && cfg.dim_head == 32 && N <= 64) {
+      // BF16_ATTN: LN + f16x3 qkv conv, the bf16-MFMA window core, f16x3 proj + residual
+      Scope sc(arena);
+      const int hid = cfg.heads * 32;
+      View ln = alloc_cf(x.B, x.C, x.T, x.H, x.W);
+      if (!plan) channel_ln(s, ln, x, nullptr, D(p + ".fn.norm.gamma"));
+      View qkv = alloc_cf(x.B, 3 * hid, x.T, x.H, x.W);
+      conv(qkv, ln, nullptr, P(p + ".fn.fn.attn.qkv.weight"), 1, 0, nullptr);
+      View o = alloc_cf(x.B, hid, x.T, x.H, x.W);
+      if (!plan)
+        REQUIRE(attention_bf16(s, qkv, o, g, cfg.heads, cfg.dim_head, bias_dense.at(p), bstride, rope_cos, rope_sin,
+                               q_scale()),
+                "bf16 STW attention launch rejected");
+      conv(x, o, nullptr, P(p + ".fn.fn.attn.proj.weight"), 1, 0, D(p + ".fn.fn.attn.proj.bias"), &x);
+      return;
+    }
     if (bstride == 32 && x3_attn_ok(x.C, N, 0)) {
       const std::string a = p + ".fn.fn.attn";
       const AttnX3W& w = packed_attn_x3(a + ".qkv.weight", a + ".proj.weight");
@@ -731,6 +750,21 @@ struct ExtdmHandle {
     const int T = x.T;
     AttnGeom g{};
     g.mode = 1; g.D = T; g.H = x.H; g.W = x.W;
+    if (bf16_attn() && cfg.dim_head == 32 && T <= 32) {
+      // BF16_ATTN: double-LN prologue, f16x3 qkv conv, bf16-MFMA core, f16x3 to_out + residual
+      Scope sc(arena);
+      const int hid = cfg.heads * 32;
+      View z = alloc_cf(x.B, x.C, T, x.H, x.W), rr = alloc_cf(x.B, x.C, T, x.H, x.W);
+      if (!plan) temporal_prologue(s, x, D(p + ".fn.norm.gamma"), D(a + ".norm.weight"), D(a + ".norm.bias"), z, rr);
+      View qkv = alloc_cf(x.B, 3 * hid, T, x.H, x.W);
+      conv(qkv, z, nullptr, P(a + ".attn.to_qkv.weight"), 1, 0, nullptr);
+      View o = alloc_cf(x.B, hid, T, x.H, x.W);
+      if (!plan)
+        REQUIRE(attention_bf16(s, qkv, o, g, cfg.heads, cfg.dim_head, time_bias, 32, rope_cos, rope_sin, q_scale()),
+                "bf16 temporal attention launch rejected");
+      conv(out, o, nullptr, P(a + ".attn.to_out.weight"), 1, 0, nullptr, &rr);
+      return;
+    }
     if (x3_attn_ok(x.C, T, 1) && out.sc == x.sc && out.st == x.st) {
       const AttnX3W& w = packed_attn_x3(a + ".attn.to_qkv.weight", a + ".attn.to_out.weight");
       if (plan) return;
@@ -847,7 +881,7 @@ struct ExtdmHandle {
     View a = alloc_cf(B, C, tp, fs, fs);
     if (!plan) {
       static const bool off = [] { const char* v = getenv("EXTDM_NO_X3_CROSS"); return v && v[0] && v[0] != '0'; }();
-      const bool x3 = !off && cfg.precision == EXTDM_PRECISION_F16X3 &&
+      const bool x3 = !off && x3_convs() &&
                       cross_attention_x3(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
       if (!x3) cross_attention(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
     }
@@ -1752,7 +1786,7 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     if (x_T) HIPCHK(hipMemcpyAsync(out, x_T, (size_t)B * n * sizeof(float), hipMemcpyDeviceToDevice, s));
     else fill_normal(s, out, B, n, seed, sample_base, round, 0x7FFFFFFF);
     HIPCHK(hipMemsetAsync(h->step_ctr, 0, sizeof(int), s));
-    if (h->cfg.precision == EXTDM_PRECISION_F16X3) x3_range_reset(s);
+    if (h->x3_convs()) x3_range_reset(s);
     h->prepare_cond(B, x_cond, cond_fea);  // t-independent cond-frame work, once per call
     int klo, khi;
     float w;
@@ -1782,7 +1816,7 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(h->ev_out, s));
     HIPCHK(hipStreamWaitEvent(caller, h->ev_out, 0));
-    REQUIRE(h->cfg.precision != EXTDM_PRECISION_F16X3 || x3_range_read(s) == 0,
+    REQUIRE(!h->x3_convs() || x3_range_read(s) == 0,
             "f16x3 precision: a conv input reached |v| >= 65504 during sampling; results are not fp32-accurate "
             "(create the handle with EXTDM_PRECISION_FP32)");
   });
@@ -1865,7 +1899,7 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     const View* in1 = c1 ? &fup : nullptr;
     X3Op op;
     if (layer == 5) {
-      REQUIRE(h->cfg.precision == EXTDM_PRECISION_F16X3 && conv_x3_op_supported(r, w, c0, 1),
+      REQUIRE(h->x3_convs() && conv_x3_op_supported(r, w, c0, 1),
               "bench layer 5: the operand-input conv is not covered (f16x3 only)");
       op.B = B; op.C = c0; op.T = T; op.H = Lq; op.W = Lq; op.pad = 1;
       op.p = reinterpret_cast<_Float16*>(h->arena.alloc((x3op_halves(B, c0, T, Lq, Lq, 1) + 1) / 2));

@@ -57,8 +57,13 @@ enum { EXTDM_SAMPLER_DDPM = 0, EXTDM_SAMPLER_DDIM = 1 };
  *   F16X3  fp32 operands split as hi + lo fp16 pairs, three fp16 MFMAs per product
  *          (lo*hi + hi*lo + hi*hi) into fp32 accumulators: fp32-level error, 5.3x
  *          the fp32 MFMA rate. Needs |activation| < 65504 at conv inputs; a value
- *          outside raises the range flag (extdm_range_flag; extdm_sample fails). */
-enum { EXTDM_PRECISION_FP32 = 0, EXTDM_PRECISION_F16X3 = 1 };
+ *          outside raises the range flag (extdm_range_flag; extdm_sample fails).
+ *   BF16_ATTN  F16X3 convolutions; the attention QK^T / PV contractions of the STW
+ *          window and temporal layers on bf16 MFMA (v_mfma_f32_32x32x16_bf16, fp32
+ *          accumulate; q, k, probabilities and v rounded to bf16), the configuration
+ *          BASELINE names for UCF-101 256. Not fp32-faithful: tests/test_gpu_bf16_attn.py
+ *          states its tolerance against the fp32 reference. */
+enum { EXTDM_PRECISION_FP32 = 0, EXTDM_PRECISION_F16X3 = 1, EXTDM_PRECISION_BF16_ATTN = 2 };
 
 typedef struct ExtdmConfig {
   int arch;            /* EXTDM_ARCH_* */

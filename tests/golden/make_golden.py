@@ -45,10 +45,12 @@ REF_MODULES = {'ada': 'DenoiseNet_STWAtt_w_w_ref_adaptor_cross_multi_traj_ada',
                'wo_ref': 'DenoiseNet_STWAtt_w_wo_ref_adaptor_cross_multi'}
 
 
-def variants():
+def variants(only=None):
     """One forward per denoiser variant: keys + eps."""
     keys = json.load(open(os.path.join(HERE, 'unet_keys.json')))
     for name in VARIANTS:
+        if only and name not in only:
+            continue
         cfg = CONFIGS[name]
         mod = importlib.import_module('model.BaseDM_adaptor.' + REF_MODULES[cfg.short])
         net = build_ref_unet(mod.Unet3D, cfg)
@@ -356,7 +358,9 @@ if __name__ == '__main__':
         torch.set_num_threads(8)
         import_reference()
         if '--variants' in sys.argv:
-            variants()
+            # --variants [name ...]: only the named variants (default: all)
+            rest = sys.argv[sys.argv.index('--variants') + 1:]
+            variants([a for a in rest if not a.startswith('--')] or None)
         if '--lfae' in sys.argv:
             lfae()
         if '--wrappers' in sys.argv:

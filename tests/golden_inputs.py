@@ -26,13 +26,17 @@ CONFIGS = {
     # ada_u22 (Cityscapes module): T = 7 pads to 8 in 4x4x4 windows
     'u22_small': _for(_spec.ARCH_ADA_U22, tc=2, tp=5, latent=16, fea_size=8),
     'u22_city': _for(_spec.ARCH_ADA_U22, tc=2, tp=5),
+    # ada_u22 at the UCF-101 256 x 256 size (BASELINE configs[4]): VideoFlowDiffusion_multi_w_ref_u22
+    # with ucf.yaml's scale 0.5 -> flow / latent 128 (diffusion image_size = 256 // 2), cond_fea =
+    # the generator bottleneck at 256 / 4 = 64; cond 4 / pred 12 (T = 16)
+    'u22_ucf': _for(_spec.ARCH_ADA_U22, tc=4, tp=12, latent=128, fea_size=64),
     # wo_ref (SMMNIST module): dims (1,2,4,8), tc-1 cond frames, cond_fea at latent size
     'woref_small': _for(_spec.ARCH_WO_REF, tc=3, tp=4, latent=16),
     'woref_smmnist': _for(_spec.ARCH_WO_REF, tc=10, tp=5),
 }
-VARIANTS = ['ada_small', 'ada_kth', 'u22_small', 'u22_city', 'woref_small', 'woref_smmnist']
+VARIANTS = ['ada_small', 'ada_kth', 'u22_small', 'u22_city', 'u22_ucf', 'woref_small', 'woref_smmnist']
 # the batch each golden forward is run at
-GOLDEN_BATCH = {'ada_kth': 1, 'u22_city': 1, 'woref_smmnist': 1}
+GOLDEN_BATCH = {'ada_kth': 1, 'u22_city': 1, 'u22_ucf': 1, 'woref_smmnist': 1}
 GEN_CFG = _spec.GeneratorConfig()
 # LFAE encoder side: bair.yaml flow_params (estimate_occlusion_map per test)
 LFAE_CFG = _spec.LfaeConfig()

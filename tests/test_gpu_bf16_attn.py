@@ -1,0 +1,50 @@
+"""EXTDM_PRECISION_BF16_ATTN (attn_bf16.hip): f16x3 convolutions with the STW / temporal
+attention QK^T and PV on bf16 MFMA — the BASELINE UCF-101 256 configuration. Not
+fp32-faithful; the stated tolerance is relative to the reference eps scale:
+
+    max |eps_bf16 - eps_ref| <= 2e-2 * max |eps_ref|
+
+(bf16 keeps 8 significant bits: q, k, the probabilities and v each carry <= 2^-9
+relative rounding; measured values are printed with -s)."""
+import importlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_inputs import CONFIGS, PKG, GOLDEN_BATCH, make_sd, unet_inputs
+
+pytestmark = pytest.mark.gpu
+pkg = importlib.import_module(PKG)
+DEV = torch.device('cuda:0')
+GOLD = os.path.join(os.path.dirname(__file__), 'golden')
+REL_TOL = 2e-2
+
+
+def _eps(name, precision):
+    cfg = CONFIGS[name]
+    B = GOLDEN_BATCH.get(name, 2)
+    x, t, cond, fea = unet_inputs(cfg, B=B)
+    h = pkg._lib.Handle(cfg, 1000, B, 0, precision=precision)
+    sd = make_sd(cfg)
+    sd.update(pkg.schedule_buffers(1000))
+    h.load_state(sd)
+    h.finalize()
+    out = torch.empty(x.shape, device=DEV)
+    h.unet_forward(x.to(DEV), t.to(DEV), cond.to(DEV), fea.to(DEV), out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize('name', ['small', 'bair', 'u22_small', 'u22_ucf'])
+def test_bf16_attention_forward_within_stated_tolerance(name):
+    g = np.load(os.path.join(GOLD, f'unet_{name}.npz'))['eps']
+    e16 = _eps(name, 'bf16_attn')
+    err = np.abs(e16 - g).max()
+    scale = np.abs(g).max()
+    print(f'{name}: bf16_attn max|err| {err:.3e} = {err / scale:.2e} x max|eps|')
+    assert np.isfinite(e16).all()
+    assert err <= REL_TOL * scale, (err, scale)
+    # and it really is a different arithmetic from the fp32-faithful mode
+    assert err > 1e-6
