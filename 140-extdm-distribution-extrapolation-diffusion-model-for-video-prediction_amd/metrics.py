@@ -144,3 +144,25 @@ def metric_stuff(metric):
     avg_metric, std_metric = metric.mean().item(), metric.std().item()
     conf95_metric = avg_metric - float(st.norm.interval(confidence=0.95, loc=avg_metric, scale=st.sem(metric))[0])
     return avg_metric, std_metric, conf95_metric
+
+
+def eval_metrics(origin_videos, result_videos, cond_frames, origin_feats=None, result_feats=None):
+    """The metric half of valid.py:199-257 on [b, n, t, c, h, w] videos: per clip the best of
+    its n samples for PSNR and SSIM over the predicted frames (calculate_psnr2 /
+    calculate_ssim2), summarised by metric_stuff. With video features given (origin [b, d],
+    result [b * n, d]; the reference's I3D features, not shipped with it), the best sample
+    per clip by feature L1 (valid.py:234-240) and its frechet_distance to the originals
+    ('fvd_best'). LPIPS needs network weights the reference does not ship: not computed."""
+    psnr_list, ssim_list = best_of_n(origin_videos, result_videos, cond_frames)
+    avg_psnr, std_psnr, conf95_psnr = metric_stuff(np.array(psnr_list))
+    avg_ssim, std_ssim, conf95_ssim = metric_stuff(np.array(ssim_list))
+    out = {'psnr': avg_psnr, 'psnr_std': std_psnr, 'psnr_conf95': conf95_psnr,
+           'ssim': avg_ssim, 'ssim_std': std_ssim, 'ssim_conf95': conf95_ssim}
+    if origin_feats is not None and result_feats is not None:
+        n = result_videos.shape[1]
+        idx = select_best(origin_feats, result_feats, n)
+        rf = np.asarray(result_feats).reshape(len(idx), n, -1)
+        best = rf[np.arange(len(idx)), idx]
+        out['fvd_best'] = frechet_distance(np.asarray(origin_feats), best)
+        out['selected_index'] = idx
+    return out

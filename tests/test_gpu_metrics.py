@@ -56,3 +56,24 @@ def test_frame_metrics_rejects_two_channels():
     a = torch.rand(1, 1, 2, 16, 16).cuda()
     with pytest.raises(ValueError):
         M.frame_metrics(a, a)
+
+
+def test_eval_metrics_summary():
+    """valid.py:226-257's reductions: best-of-n per clip, then metric_stuff; fvd_best from
+    the feature-L1 selection."""
+    from tests.golden_inputs import metric_feats
+    a, b = metric_videos('rgb')
+    orig = torch.stack([a, a.flip(0), a])
+    res = torch.stack([b, b.flip(0), b.flip(1)])
+    fake, real = metric_feats()
+    ofeat, rfeat = real[:3].astype(np.float64), np.concatenate([fake[:9]]).astype(np.float64)
+    out = M.eval_metrics(orig.cuda(), res.cuda(), 1, ofeat, rfeat)
+    ps = []
+    for i in range(3):
+        p, _ = mo.frame_metrics(orig[i, :, 1:].numpy(), res[i, :, 1:].numpy())
+        ps.append(np.max(p.mean(-1)))
+    assert out['psnr'] == pytest.approx(np.mean(ps), abs=1e-9)
+    assert out['psnr_std'] == pytest.approx(np.std(ps), abs=1e-9)
+    idx = M.select_best(ofeat, rfeat, 3)
+    best = rfeat.reshape(3, 3, -1)[np.arange(3), idx]
+    assert out['fvd_best'] == pytest.approx(M.frechet_distance(ofeat, best), rel=1e-12)
