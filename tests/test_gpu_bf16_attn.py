@@ -2,10 +2,11 @@
 attention QK^T and PV on bf16 MFMA — the BASELINE UCF-101 256 configuration. Not
 fp32-faithful; the stated tolerance is relative to the reference eps scale:
 
-    max |eps_bf16 - eps_ref| <= 2e-2 * max |eps_ref|
+    max |eps_bf16 - eps_ref| <= 5e-3 * max |eps_ref|
 
 (bf16 keeps 8 significant bits: q, k, the probabilities and v each carry <= 2^-9
-relative rounding; measured values are printed with -s)."""
+relative rounding). Measured (MI355X, round 2): 2.05e-3 (u12 reduced), 1.50e-3 (BAIR),
+1.43e-3 (ada_u22 reduced), 8.9e-4 (UCF-101 256) x max|eps|; printed with -s."""
 import importlib
 import os
 
@@ -19,7 +20,7 @@ pytestmark = pytest.mark.gpu
 pkg = importlib.import_module(PKG)
 DEV = torch.device('cuda:0')
 GOLD = os.path.join(os.path.dirname(__file__), 'golden')
-REL_TOL = 2e-2
+REL_TOL = 5e-3
 
 
 def _eps(name, precision):
