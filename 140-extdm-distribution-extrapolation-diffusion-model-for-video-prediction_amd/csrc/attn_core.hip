@@ -1,16 +1,22 @@
-// bf16-MFMA attention core for EXTDM_PRECISION_BF16_ATTN (the UCF-101 256 configuration
-// of BASELINE: "bf16 MFMA attention"): the QK^T and PV contractions of
+// Attention core (the QK^T and PV contractions on qkv produced by a 1x1 conv) of
 //   STW window self-attention    WindowAttention3D + STWAttentionLayer, u12:408-559
 //                                (shifted 3-D windows of <= 64 tokens: ada / ada_u22 4x4x4)
 //   temporal attention per pixel Attention, u12:252-302 (<= 32 frames)
-// on v_mfma_f32_32x32x16_bf16 with fp32 accumulation; everything around them (the qkv /
-// proj 1x1 convs, LayerNorms, residuals) stays f16x3 / fp32.
+// in two arithmetics (template X3):
+//   X3 = true   f16x3 (hi / lo fp16 operands, three v_mfma_f32_32x32x16_f16 per product,
+//               fp32-faithful; conv_x3.hip): the F16X3 path for the shapes the fused
+//               kernels do not cover (C = 256 windows, 64-token windows)
+//   X3 = false  bf16 (v_mfma_f32_32x32x16_bf16): EXTDM_PRECISION_BF16_ATTN, the UCF-101 256
+//               configuration of BASELINE ("bf16 MFMA attention")
+// Everything around the core (LayerNorms, the qkv / proj 1x1 convs, residuals) runs as f16x3.
 //
-// One wave per (token group, head), up to 64 tokens as two 32-token tiles:
+// One wave per (token group, head); a group is NT 32-token tiles: NT = 2 for 64-token
+// windows, NT = 1 for windows of <= 32 tokens and for temporal groups (32 / T' pixels'
+// frames, T' = 16 or 32 slots), so no block of the score matrix is wholly masked.
 //   lane = (token column c = lane & 31, half h = lane >> 5); an operand fragment holds the
 //   8 dims 16s + 8h .. +7 of k-step s (dim_head 32: s = 0, 1), so rotary pairs stay in-lane.
-//   S^T[kt][qt] = K[kt] Q[qt]^T   (4 tiles x 2 k-steps): a lane holds 16 keys of its query
-//   softmax over the 64 keys: in-lane over (kt, r), then the partner half (lane ^ 32)
+//   S^T[kt][qt] = K[kt] Q[qt]^T   (NT^2 tiles x 2 k-steps): a lane holds 16 keys of its query
+//   softmax over the keys: in-lane over (kt, r), then the partner half (lane ^ 32)
 //   O^T[qt]    += V^T P^T         P^T straight from the score registers as the B operand
 //   (k-step = registers 8s'..8s'+7 of one key tile, keys in the accumulator's row order);
 //   V^T is read from an LDS copy of V in that same key order.
@@ -24,6 +30,40 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+// operand fragment of 8 k-elements: bf16, or the f16x3 hi / lo pair
+template <bool X3> struct Frag;
+template <> struct Frag<false> {
+  bf8 v;
+  __device__ void set(const float* x, int& bad) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (__bf16)x[e];
+    (void)bad;
+  }
+};
+template <> struct Frag<true> {
+  h8 hi, lo;
+  __device__ void set(const float* x, int& bad) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float w = split_src(x[e]);
+      bad |= fabsf(w) >= 65504.f;
+      const _Float16 a = (_Float16)w;
+      hi[e] = a;
+      lo[e] = (_Float16)(w - (float)a);
+    }
+  }
+};
+// c += A * B (rows of A x columns of B over 16 k)
+__device__ __forceinline__ f32x16 mma(const Frag<false>& a, const Frag<false>& b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v, b.v, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mma(const Frag<true>& a, const Frag<true>& b, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.lo, b.hi, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.lo, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.hi, c, 0, 0, 0);
+}
 
 __device__ __forceinline__ int dof(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -39,10 +79,10 @@ struct TokB {
   int valid, exists, lab, rpos;
 };
 
-// token tk (0..63) of group grp: its position, whether it is a real in-image token,
-// its shifted-window region label (MODE 0) or pixel slot (MODE 1), and its rotary /
+// token tk (0 .. 32 NT - 1) of group grp: its position, whether it is a real in-image
+// token, its shifted-window region label (MODE 0) or pixel slot (MODE 1), and its rotary /
 // bias position (window token index, or frame)
-template <int MODE>
+template <int MODE, int NT>
 __device__ __forceinline__ TokB token_b(int tk, const AttnGeom& g, long st, int grp, int per) {
   TokB o;
   if (MODE == 0) {
@@ -64,7 +104,7 @@ __device__ __forceinline__ TokB token_b(int tk, const AttnGeom& g, long st, int 
   } else {
     const int HW = g.H * g.W;
     const int p = tk / per, t = tk % per;
-    const int hw = grp * (64 / per) + p;
+    const int hw = grp * (32 * NT / per) + p;
     o.exists = t < g.D && hw < HW;
     o.valid = o.exists;
     o.pos = (long)t * st + (o.exists ? hw : 0);
@@ -74,62 +114,63 @@ __device__ __forceinline__ TokB token_b(int tk, const AttnGeom& g, long st, int 
   return o;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256) void attn_bf16_kernel(const float* __restrict__ qkv, long qsb, long qsc, long st,
+template <int MODE, bool X3, int NT>
+__global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict__ qkv, long qsb, long qsc, long st,
                                                         float* __restrict__ o, long osb, long osc, AttnGeom g,
                                                         int heads, int groups_per_sample, int total_groups,
                                                         const float* __restrict__ bias_dense, int bstride,
                                                         const float* __restrict__ rcos,
-                                                        const float* __restrict__ rsin, float q_scale) {
-  __shared__ float Vs[4][64][33];
+                                                        const float* __restrict__ rsin, float q_scale,
+                                                        int* __restrict__ range_flag) {
+  __shared__ float Vs[4][32 * NT][33];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
   // a block = one token group, its waves walk the heads
   const int gidx = blockIdx.x;
   if (gidx >= total_groups) return;
   const int b = gidx / groups_per_sample, grp = gidx % groups_per_sample;
-  const int per = g.D <= 16 ? 16 : 32;  // MODE 1: frames slot per pixel
-  const TokB tq[2] = {token_b<MODE>(c, g, st, grp, per), token_b<MODE>(32 + c, g, st, grp, per)};
+  const int per = g.D <= 16 ? 16 : 32;  // MODE 1: frame slots per pixel
+  TokB tq[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) tq[t] = token_b<MODE, NT>(32 * t + c, g, st, grp, per);
   const int hid = heads * 32;
   const float* qb = qkv + (long)b * qsb;
   const bool shifted = MODE == 0 && (g.ss0 | g.ss1 | g.ss2) != 0;
   // masks of the 16 keys a lane's score registers hold, per (query tile, key tile): bit r
   // of neg[qt][kt] = -inf (padded key, or another pixel's frame), of mis[qt][kt] = -100
   // (shifted-window region mismatch)
-  unsigned neg[2][2] = {{0u, 0u}, {0u, 0u}}, mis[2][2] = {{0u, 0u}, {0u, 0u}};
+  unsigned neg[NT][NT], mis[NT][NT];
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+  for (int kt = 0; kt < NT; ++kt) {
+#pragma unroll
+    for (int qt = 0; qt < NT; ++qt) neg[qt][kt] = mis[qt][kt] = 0u;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const TokB kk = token_b<MODE>(kt * 32 + dof(r, h), g, st, grp, per);
+      const TokB kk = token_b<MODE, NT>(kt * 32 + dof(r, h), g, st, grp, per);
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+      for (int qt = 0; qt < NT; ++qt) {
         const bool other = kk.lab != tq[qt].lab;
         neg[qt][kt] |= (unsigned)(!kk.exists || (MODE == 1 && other)) << r;
         mis[qt][kt] |= (unsigned)(MODE == 0 && shifted && other) << r;
       }
     }
+  }
+  int bad = 0;
   for (int hd = wave; hd < heads; hd += 4) {
     // ---- Q, K fragments (token per lane, 16 dims each), rotary in-lane, V to LDS ----
-    bf8 qf[2][2], kf[2][2];  // [tile][k-step]
+    Frag<X3> qf[NT][2], kf[NT][2];  // [tile][k-step]
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < NT; ++t) {
       float qv[16], kv[16];
+      const bool ok = tq[t].valid;
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int d = 16 * s + 8 * h + e;
-          const bool ok = tq[t].valid;
           qv[8 * s + e] = ok ? qb[(long)(hd * 32 + d) * qsc + tq[t].pos] : 0.f;
           kv[8 * s + e] = ok ? qb[(long)(hid + hd * 32 + d) * qsc + tq[t].pos] : 0.f;
-        }
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int d = 16 * s + 8 * h + e;
-          Vs[wave][t * 32 + c][d] = tq[t].valid ? qb[(long)(2 * hid + hd * 32 + d) * qsc + tq[t].pos] : 0.f;
+          Vs[wave][t * 32 + c][d] = ok ? qb[(long)(2 * hid + hd * 32 + d) * qsc + tq[t].pos] : 0.f;
         }
 #pragma unroll
       for (int s = 0; s < 2; ++s)
@@ -145,105 +186,113 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(const float* __restrict_
           kv[8 * s + e + 1] = k1 * cs + k0 * sn;
         }
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          qf[t][s][e] = (__bf16)qv[8 * s + e];
-          kf[t][s][e] = (__bf16)kv[8 * s + e];
-        }
+      for (int s = 0; s < 2; ++s) {
+        qf[t][s].set(qv + 8 * s, bad);
+        kf[t][s].set(kv + 8 * s, bad);
+      }
     }
     __syncthreads();  // Vs of this head visible to the wave's V^T reads (and to nobody else)
-    // ---- scores S^T[kt][qt], softmax over the keys of each query ----
-    f32x16 sc[2][2];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
+    for (int qt = 0; qt < NT; ++qt) {
+      // ---- scores S^T[kt] of query tile qt, softmax over the keys of each query ----
+      f32x16 sc[NT];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
+      for (int kt = 0; kt < NT; ++kt) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sc[kt][qt][r] = 0.f;
+        for (int r = 0; r < 16; ++r) sc[kt][r] = 0.f;
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
-          sc[kt][qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][s], qf[qt][s], sc[kt][qt], 0, 0, 0);
+        for (int s = 0; s < 2; ++s) sc[kt] = mma(kf[kt][s], qf[qt][s], sc[kt]);
       }
-    f32x16 out[2];
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
       const TokB& me = tq[qt];
       const float* bd = bias_dense + ((long)hd * bstride + me.rpos) * bstride;
       float mx = -INFINITY;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int kpos = kt * 32 + dof(r, h);  // key token; its bias column
-          float sv = sc[kt][qt][r] + bd[MODE == 0 ? kpos : kpos % per];
+          float sv = sc[kt][r] + bd[MODE == 0 ? kpos : kpos % per];
           if ((mis[qt][kt] >> r) & 1) sv += -100.f;
           if ((neg[qt][kt] >> r) & 1) sv = -INFINITY;
-          sc[kt][qt][r] = sv;
+          sc[kt][r] = sv;
           mx = fmaxf(mx, sv);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32));
       float sum = 0.f;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = expf(sc[kt][qt][r] - mx);
-          sc[kt][qt][r] = p;
+          const float p = expf(sc[kt][r] - mx);
+          sc[kt][r] = p;
           sum += p;
         }
       sum += __shfl_xor(sum, 32);
       const float inv = 1.f / sum;
-      // ---- O^T[qt] = V^T P^T over 4 k-steps of 16 keys ----
+      // ---- O^T = V^T P^T over 2 NT k-steps of 16 keys ----
+      f32x16 out;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) out[qt][r] = 0.f;
+      for (int r = 0; r < 16; ++r) out[r] = 0.f;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-          bf8 pf, vf;
+          float pv[8], vv[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            pf[e] = (__bf16)(sc[kt][qt][8 * s + e] * inv);
-            vf[e] = (__bf16)Vs[wave][kt * 32 + dof(8 * s + e, h)][c];
+            pv[e] = sc[kt][8 * s + e] * inv;
+            vv[e] = Vs[wave][kt * 32 + dof(8 * s + e, h)][c];
           }
-          out[qt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, out[qt], 0, 0, 0);
+          Frag<X3> pf, vf;
+          pf.set(pv, bad);
+          vf.set(vv, bad);
+          out = mma(vf, pf, out);
         }
-    }
-    // out[qt][r] = O[query qt*32 + c][dim dof(r, h)]
+      // out[r] = O[query qt*32 + c][dim dof(r, h)]
+      if (me.valid) {
+        float* ob = o + (long)b * osb + me.pos;
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      if (!tq[qt].valid) continue;
-      float* ob = o + (long)b * osb + tq[qt].pos;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ob[(long)(hd * 32 + dof(r, h)) * osc] = out[qt][r];
+        for (int r = 0; r < 16; ++r) ob[(long)(hd * 32 + dof(r, h)) * osc] = out[r];
+      }
     }
     __syncthreads();  // Vs reuse by the next head
   }
+  if (X3 && bad) atomicOr(range_flag, 2);
 }
 
 }  // namespace
 
-bool attention_bf16(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads, int dim_head,
-                    const float* bias_dense, int bstride, const float* rope_cos, const float* rope_sin,
-                    float q_scale) {
+bool attention_core(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads, int dim_head,
+                    const float* bias_dense, int bstride, const float* rope_cos, const float* rope_sin, float q_scale,
+                    bool bf16) {
   if (dim_head != 32 || qkv.st != o.st) return false;
-  int groups;
+  int groups, nt = 1;
   if (g.mode == 0) {
-    if (g.ws0 * g.ws1 * g.ws2 > 64) return false;
+    const int N = g.ws0 * g.ws1 * g.ws2;
+    if (N > 64) return false;
+    nt = N > 32 ? 2 : 1;
     groups = (g.Dp / g.ws0) * (g.Hp / g.ws1) * (g.Wp / g.ws2);
   } else {
     if (g.D > 32) return false;
-    const int ppw = 64 / (g.D <= 16 ? 16 : 32);
+    const int ppw = 32 / (g.D <= 16 ? 16 : 32);  // pixels per 32-token group
     groups = (g.H * g.W + ppw - 1) / ppw;
   }
   const int total = qkv.B * groups;
-  if (g.mode == 0)
-    hipLaunchKernelGGL(attn_bf16_kernel<0>, dim3(total), dim3(256), 0, s, qkv.p, qkv.sb, qkv.sc, qkv.st, o.p, o.sb,
-                       o.sc, g, heads, groups, total, bias_dense, bstride, rope_cos, rope_sin, q_scale);
-  else
-    hipLaunchKernelGGL(attn_bf16_kernel<1>, dim3(total), dim3(256), 0, s, qkv.p, qkv.sb, qkv.sc, qkv.st, o.p, o.sb,
-                       o.sc, g, heads, groups, total, bias_dense, bstride, rope_cos, rope_sin, q_scale);
+  int* flag = x3_range_ptr();
+#define CORE_GO(M, X, NT_)                                                                                   \
+  hipLaunchKernelGGL((attn_core_kernel<M, X, NT_>), dim3(total), dim3(256), 0, s, qkv.p, qkv.sb, qkv.sc, qkv.st,  \
+                     o.p, o.sb, o.sc, g, heads, groups, total, bias_dense, bstride, rope_cos, rope_sin, q_scale, flag)
+  if (g.mode == 0 && nt == 2) {
+    if (bf16) CORE_GO(0, false, 2);
+    else CORE_GO(0, true, 2);
+  } else if (g.mode == 0) {
+    if (bf16) CORE_GO(0, false, 1);
+    else CORE_GO(0, true, 1);
+  } else {
+    if (bf16) CORE_GO(1, false, 1);
+    else CORE_GO(1, true, 1);
+  }
+#undef CORE_GO
   return true;
 }
 

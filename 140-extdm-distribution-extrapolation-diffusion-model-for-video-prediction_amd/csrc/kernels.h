@@ -150,12 +150,13 @@ struct AttnGeom {
   int ss0, ss1, ss2; // effective shift
   int Dp, Hp, Wp;    // padded extents
 };
-// bf16-MFMA attention core (attn_bf16.hip, EXTDM_PRECISION_BF16_ATTN): same operands and
-// geometry as window_attention, groups of <= 64 tokens (temporal: <= 32 frames), dim_head 32;
-// false if the shape is not covered. bias_dense [heads][bstride][bstride].
-bool attention_bf16(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads, int dim_head,
-                    const float* bias_dense, int bstride, const float* rope_cos, const float* rope_sin,
-                    float q_scale);
+// Attention core (attn_core.hip): QK^T / softmax / PV over qkv [B][3*heads*32][T][H][W]
+// into o [B][heads*32][T][H][W], token groups of <= 64 (temporal: <= 32 frames),
+// dim_head 32; f16x3 (fp32-faithful) or bf16 (EXTDM_PRECISION_BF16_ATTN). False if the
+// shape is not covered. bias_dense [heads][bstride][bstride].
+bool attention_core(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads, int dim_head,
+                    const float* bias_dense, int bstride, const float* rope_cos, const float* rope_sin, float q_scale,
+                    bool bf16);
 // Unfused attention (dim_head 32, <= 32 tokens per group; e.g. C = 512 levels).
 // qkv: channel-first [B][3*heads*32][T][H][W]; o: [B][heads*32][T][H][W].
 void window_attention(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads,

@@ -682,6 +682,15 @@ struct ExtdmHandle {
     static const bool off = [] { const char* v = getenv("EXTDM_NO_FUSED_STW"); return v && v[0] && v[0] != '0'; }();
     return !off && fused_attn_supported(C, ntok, cfg.dim_head, cfg.heads);
   }
+  // the unfused core path (LN -> qkv 1x1 conv -> attn_core.hip -> proj 1x1 conv + residual):
+  // always in BF16_ATTN; in F16X3 for the shapes the fused f16x3 kernels do not cover
+  // (C = 256 windows, 64-token windows) unless EXTDM_NO_X3_CORE sends them to the fp32 fused kernels
+  bool core_attn(int ntok, int max_tok, bool fused_x3) const {
+    if (cfg.dim_head != 32 || ntok > max_tok) return false;
+    if (bf16_attn()) return true;
+    static const bool off = [] { const char* v = getenv("EXTDM_NO_X3_CORE"); return v && v[0] && v[0] != '0'; }();
+    return cfg.precision == EXTDM_PRECISION_F16X3 && !fused_x3 && !off;
+  }
   float q_scale() const { return 1.0f / std::sqrt((float)cfg.dim_head); }
   // model frame count: wo_ref drops the last cond frame (wo_ref.py:911)
   int tm() const { return cfg.arch == EXTDM_ARCH_WO_REF ? cfg.tc - 1 : cfg.tc; }
@@ -694,8 +703,9 @@ struct ExtdmHandle {
     // dense bias tables are laid out for the configured window (build_tables); a
     // collapsed window reads their leading N x N block (index[:N, :N], u12:476)
     const int bstride = cfg.window[0] * cfg.window[1] * cfg.window[2] <= 32 ? 32 : 64;
-    if (bf16_attn() && cfg.dim_head == 32 && N <= 64) {
-      // BF16_ATTN: LN + f16x3 qkv conv, the bf16-MFMA window core, f16x3 proj + residual
+    const bool fused_x3 = bstride == 32 && x3_attn_ok(x.C, N, 0);
+    if (core_attn(N, 64, fused_x3)) {
+      // LN + f16x3 qkv conv, the window core (bf16 or f16x3 MFMA), f16x3 proj + residual
       Scope sc(arena);
       const int hid = cfg.heads * 32;
       View ln = alloc_cf(x.B, x.C, x.T, x.H, x.W);
@@ -704,13 +714,13 @@ struct ExtdmHandle {
       conv(qkv, ln, nullptr, P(p + ".fn.fn.attn.qkv.weight"), 1, 0, nullptr);
       View o = alloc_cf(x.B, hid, x.T, x.H, x.W);
       if (!plan)
-        REQUIRE(attention_bf16(s, qkv, o, g, cfg.heads, cfg.dim_head, bias_dense.at(p), bstride, rope_cos, rope_sin,
-                               q_scale()),
-                "bf16 STW attention launch rejected");
+        REQUIRE(attention_core(s, qkv, o, g, cfg.heads, cfg.dim_head, bias_dense.at(p), bstride, rope_cos, rope_sin,
+                               q_scale(), bf16_attn()),
+                "STW attention core launch rejected");
       conv(x, o, nullptr, P(p + ".fn.fn.attn.proj.weight"), 1, 0, D(p + ".fn.fn.attn.proj.bias"), &x);
       return;
     }
-    if (bstride == 32 && x3_attn_ok(x.C, N, 0)) {
+    if (fused_x3) {
       const std::string a = p + ".fn.fn.attn";
       const AttnX3W& w = packed_attn_x3(a + ".qkv.weight", a + ".proj.weight");
       if (plan) return;
@@ -750,8 +760,9 @@ struct ExtdmHandle {
     const int T = x.T;
     AttnGeom g{};
     g.mode = 1; g.D = T; g.H = x.H; g.W = x.W;
-    if (bf16_attn() && cfg.dim_head == 32 && T <= 32) {
-      // BF16_ATTN: double-LN prologue, f16x3 qkv conv, bf16-MFMA core, f16x3 to_out + residual
+    const bool fused_x3 = x3_attn_ok(x.C, T, 1) && out.sc == x.sc && out.st == x.st;
+    if (core_attn(T, 32, fused_x3)) {
+      // double-LN prologue, f16x3 qkv conv, the core (bf16 or f16x3 MFMA), f16x3 to_out + residual
       Scope sc(arena);
       const int hid = cfg.heads * 32;
       View z = alloc_cf(x.B, x.C, T, x.H, x.W), rr = alloc_cf(x.B, x.C, T, x.H, x.W);
@@ -760,12 +771,13 @@ struct ExtdmHandle {
       conv(qkv, z, nullptr, P(a + ".attn.to_qkv.weight"), 1, 0, nullptr);
       View o = alloc_cf(x.B, hid, T, x.H, x.W);
       if (!plan)
-        REQUIRE(attention_bf16(s, qkv, o, g, cfg.heads, cfg.dim_head, time_bias, 32, rope_cos, rope_sin, q_scale()),
-                "bf16 temporal attention launch rejected");
+        REQUIRE(attention_core(s, qkv, o, g, cfg.heads, cfg.dim_head, time_bias, 32, rope_cos, rope_sin, q_scale(),
+                               bf16_attn()),
+                "temporal attention core launch rejected");
       conv(out, o, nullptr, P(a + ".attn.to_out.weight"), 1, 0, nullptr, &rr);
       return;
     }
-    if (x3_attn_ok(x.C, T, 1) && out.sc == x.sc && out.st == x.st) {
+    if (fused_x3) {
       const AttnX3W& w = packed_attn_x3(a + ".attn.to_qkv.weight", a + ".attn.to_out.weight");
       if (plan) return;
       REQUIRE(temporal_x3(s, x, out, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), D(a + ".norm.weight"),

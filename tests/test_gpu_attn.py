@@ -1,5 +1,7 @@
 """GPU: single attention layers (extdm_attn_layer) against the CPU oracle — STW window
-attention (shifted / unshifted) and temporal attention, in both precisions.
+attention (shifted / unshifted) and temporal attention, in both precisions. BAIR levels
+0-1 (C = 64 / 128) run the fused f16x3 kernels (stw_x3.hip) in F16X3, level 2 (C = 256)
+the unfused route with the f16x3 attention core (attn_core.hip).
 Bar: max-abs <= 2e-5 on the layer output (|out| ~ 1-4; fp32 reference drift ~1e-6)."""
 import importlib
 

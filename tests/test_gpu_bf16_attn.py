@@ -1,4 +1,4 @@
-"""EXTDM_PRECISION_BF16_ATTN (attn_bf16.hip): f16x3 convolutions with the STW / temporal
+"""EXTDM_PRECISION_BF16_ATTN (attn_core.hip, bf16 operands): f16x3 convolutions with the STW / temporal
 attention QK^T and PV on bf16 MFMA — the BASELINE UCF-101 256 configuration. Not
 fp32-faithful; the stated tolerance is relative to the reference eps scale:
 
