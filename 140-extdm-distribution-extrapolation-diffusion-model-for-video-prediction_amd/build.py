@@ -1,9 +1,10 @@
 """Build libextdm_hip.so (gfx950) in-tree with hipcc: the .so travels with the
 repository snapshot to the GPU box. No torch extension machinery is involved.
 
-`build(variant=..., opt=..., extra=...)` builds an A/B copy of the library into
-_variants/<variant>/ (per-file optimisation levels / extra flags) for the GPU
-measurement scripts (EXTDM_LIB selects it at run time)."""
+`build(variant=..., opt=..., extra=..., csrc=...)` builds an A/B copy of the library
+into _variants/<variant>/ (per-file optimisation levels / extra flags, or the sources of
+another revision in csrc) for the GPU measurement scripts (EXTDM_LIB selects it at run
+time)."""
 import os
 import subprocess
 import sys
@@ -29,21 +30,22 @@ OPT = {}
 def _needs(obj, src):
     if not os.path.exists(obj):
         return True
-    deps = [src, os.path.join(CSRC, 'kernels.h'), os.path.join(INCLUDE, 'extdm.h'), os.path.abspath(__file__)]
+    deps = [src, os.path.join(os.path.dirname(src), 'kernels.h'), os.path.join(INCLUDE, 'extdm.h'), os.path.abspath(__file__)]
     return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 
-def _compile(src, objdir, opt, per_file, extra):
+def _compile(src, objdir, opt, per_file, extra, csrc=CSRC):
     obj = os.path.join(objdir, src + '.o')
-    s = os.path.join(CSRC, src)
+    s = os.path.join(csrc, src)
     if _needs(obj, s):
-        flags = [opt.get(src, f) if f == '-O3' else f for f in FLAGS] + per_file.get(src, []) + extra.get(src, [])
+        flags = [opt.get(src, f) if f == '-O3' else (csrc if f == CSRC else f) for f in FLAGS]
+        flags += per_file.get(src, []) + extra.get(src, [])
         cmd = [HIPCC] + flags + (['-x', 'hip'] if src.endswith('.cpp') else []) + ['-c', s, '-o', obj]
         subprocess.run(cmd, check=True)
     return obj
 
 
-def build(verbose=False, variant=None, opt=None, per_file=None, extra=None):
+def build(verbose=False, variant=None, opt=None, per_file=None, extra=None, csrc=None):
     if variant:
         objdir = os.path.join(REPO, '_variants', variant, 'obj')
         lib = os.path.join(REPO, '_variants', variant, 'libextdm_hip.so')
@@ -55,7 +57,7 @@ def build(verbose=False, variant=None, opt=None, per_file=None, extra=None):
     os.makedirs(objdir, exist_ok=True)
     jobs = int(os.environ.get('MAX_JOBS', '8'))
     with ThreadPoolExecutor(max_workers=min(jobs, len(SOURCES))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, objdir, opt, per_file, extra), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, objdir, opt, per_file, extra, csrc or CSRC), SOURCES))
     if not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in objs):
         subprocess.run([HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', lib] + objs, check=True)
     if verbose:

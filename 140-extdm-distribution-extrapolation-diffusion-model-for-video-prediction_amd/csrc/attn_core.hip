@@ -36,6 +36,7 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 template <bool X3> struct Frag;
 template <> struct Frag<false> {
   bf8 v;
+  template <bool CHECK = true>
   __device__ void set(const float* x, int& bad) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = (__bf16)x[e];
@@ -44,15 +45,21 @@ template <> struct Frag<false> {
 };
 template <> struct Frag<true> {
   h8 hi, lo;
+  // CHECK: OR |x| >= 65504 (fp16 overflow of hi) into bad; probabilities skip it. Plain
+  // C++ (not the split2 asm of kernels.h): the fragments feed MFMAs, and only
+  // compiler-visible VALU gets its MFMA hazard waits.
+  template <bool CHECK = true>
   __device__ void set(const float* x, int& bad) {
+    float m = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float w = split_src(x[e]);
-      bad |= fabsf(w) >= 65504.f;
+      if (CHECK) m = fmaxf(m, fabsf(w));
       const _Float16 a = (_Float16)w;
       hi[e] = a;
       lo[e] = (_Float16)(w - (float)a);
     }
+    if (CHECK) bad |= m >= 65504.f;
   }
 };
 // c += A * B (rows of A x columns of B over 16 k)
@@ -218,12 +225,14 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
           mx = fmaxf(mx, sv);
         }
       mx = fmaxf(mx, __shfl_xor(mx, 32));
+      // exp(s - mx) as v_exp_f32 (2^x) of fma(s, log2 e, -mx log2 e): masked -inf -> 0
+      const float mxl = mx * 1.44269504088896341f;
       float sum = 0.f;
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = expf(sc[kt][r] - mx);
+          const float p = __builtin_amdgcn_exp2f(fmaf(sc[kt][r], 1.44269504088896341f, -mxl));
           sc[kt][r] = p;
           sum += p;
         }
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
             vv[e] = Vs[wave][kt * 32 + dof(8 * s + e, h)][c];
           }
           Frag<X3> pf, vf;
-          pf.set(pv, bad);
+          pf.template set<false>(pv, bad);
           vf.set(vv, bad);
           out = mma(vf, pf, out);
         }

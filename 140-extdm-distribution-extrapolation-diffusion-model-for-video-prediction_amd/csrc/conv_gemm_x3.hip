@@ -139,15 +139,16 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
 #pragma unroll
     for (int g2 = 0; g2 < 2; ++g2) {
       const int g = kg + 2 * g2;  // 8-k group: step g >> 1, half g & 1
-      h8 hi, lo;
+      unsigned hw[4], lw[4];
+      float am = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float v = split_src(breg[g2][e]);
-        bad |= fabsf(v) >= 65504.f;
-        const _Float16 x = (_Float16)v;
-        hi[e] = x;
-        lo[e] = (_Float16)(v - (float)x);
+      for (int e = 0; e < 4; ++e) {
+        split2(breg[g2][2 * e], breg[g2][2 * e + 1], hw[e], lw[e]);
+        amax2(am, breg[g2][2 * e], breg[g2][2 * e + 1]);
       }
+      bad |= am >= 65504.f;
+      const h8 hi = __builtin_bit_cast(h8, u32x4{hw[0], hw[1], hw[2], hw[3]});
+      const h8 lo = __builtin_bit_cast(h8, u32x4{lw[0], lw[1], lw[2], lw[3]});
       _Float16* d = Bs + ((g >> 1) * BN + col) * 16 + 8 * ((g & 1) ^ ((col >> 3) & 1));
       *reinterpret_cast<h8*>(d) = hi;
       *reinterpret_cast<h8*>(d + 2 * BN * 16) = lo;

@@ -248,24 +248,30 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
 #pragma unroll
     for (int j = 0; j < NSLOT; ++j) {
       if (!SPAN && sg[j] < 0) continue;
-      h8 hi0, hi1, lo0, lo1;
+      float v[16];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const float m0 = SPAN ? xmask(j, cgb, c) : 1.f, m1 = SPAN ? xmask(j, cgb, c + 8) : 1.f;
-        float r0 = xr[j][c], r1 = xr[j][c + 8];
+      for (int c = 0; c < 16; ++c) {
+        float r = xr[j][c];
         if (SPAN) {
           // pinned here (volatile: not hoisted above the stage barriers of the 7x7
           // ky loop, where the first use of a load result would wait for the X loads)
-          asm volatile("" : "+v"(r0));
-          asm volatile("" : "+v"(r1));
+          asm volatile("" : "+v"(r));
+          r *= xmask(j, cgb, c);
         }
-        const float v0 = split_src(r0 * m0), v1 = split_src(r1 * m1);
-        range_bad |= (fabsf(v0) >= 65504.f) | (fabsf(v1) >= 65504.f);
-        const _Float16 a0 = (_Float16)v0, a1 = (_Float16)v1;
-        hi0[c] = a0; hi1[c] = a1;
-        lo0[c] = (_Float16)(v0 - (float)a0);
-        lo1[c] = (_Float16)(v1 - (float)a1);
+        v[c] = r;
       }
+      unsigned hw[8], lw[8];
+      float am = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        split2(v[2 * c], v[2 * c + 1], hw[c], lw[c]);
+        amax2(am, v[2 * c], v[2 * c + 1]);
+      }
+      range_bad |= am >= 65504.f;
+      const h8 hi0 = __builtin_bit_cast(h8, u32x4{hw[0], hw[1], hw[2], hw[3]});
+      const h8 hi1 = __builtin_bit_cast(h8, u32x4{hw[4], hw[5], hw[6], hw[7]});
+      const h8 lo0 = __builtin_bit_cast(h8, u32x4{lw[0], lw[1], lw[2], lw[3]});
+      const h8 lo1 = __builtin_bit_cast(h8, u32x4{lw[4], lw[5], lw[6], lw[7]});
       const int sw = (spos[j] >> 3) & 1;
       const bool used = sg[j] >= 0;
       _Float16* dh = used ? Xs + ((long)sg[j] * a.XPOS + spos[j]) * 16 : xdummy;

@@ -150,11 +150,13 @@ __global__ __launch_bounds__(256) void cross_attn_x3_kernel(const float* __restr
       cm = fmaxf(cm, __shfl_xor(cm, 32));
       const float mn = fmaxf(m, cm);
       if (mn == -INFINITY) continue;  // a fully padded tail (never the first tile)
-      const float alpha = expf(m - mn);
+      // exp(x - mn) as v_exp_f32 (2^x) of fma(x, log2 e, -mn log2 e); exp(-inf) = 0
+      const float mnl = mn * 1.44269504088896341f;
+      const float alpha = __builtin_amdgcn_exp2f(fmaf(m, 1.44269504088896341f, -mnl));
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        sh[r] = expf(sh[r] - mn);
+        sh[r] = __builtin_amdgcn_exp2f(fmaf(sh[r], 1.44269504088896341f, -mnl));
         ps += sh[r];
       }
       ps += __shfl_xor(ps, 32);

@@ -20,6 +20,30 @@ __device__ __forceinline__ float split_src(float v) {
   return v;
 }
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// f16x3 split of two fp32 values in one opaque block: hi = fp16_rn(v) packed, lo =
+// fp16_rn(v - hi) packed; v - hi is exact and v_fma_mix_f32 reads hi straight from the
+// packed fp16 register (4 VALU per pair instead of ~5.3 for the converted-back hi, and the
+// two roundings cannot be lowered differently, cf. split_src). For operands staged through LDS only:
+// hipcc's hazard recognizer does not see inside inline asm, so neither may read an MFMA
+// result or feed an MFMA directly (a stw_x3 version that split the PV accumulator this way
+// read it before the MFMA had written it: run-to-run differences)
+__device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned& lo) {
+  float da, db;
+  asm("v_cvt_pk_f16_f32 %0, %4, %5\n\t"
+      "v_fma_mix_f32 %2, -%0, 1.0, %4 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %3, -%0, 1.0, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_cvt_pk_f16_f32 %1, %2, %3"
+      : "=&v"(hi), "=v"(lo), "=&v"(da), "=&v"(db)
+      : "v"(a), "v"(b));
+}
+// m = max(m, |a|, |b|) in one v_max3_f32 (the fp16-range check of the split values;
+// the same hazard rule as split2)
+__device__ __forceinline__ void amax2(float& m, float a, float b) {
+  asm("v_max3_f32 %0, |%1|, |%2|, %0" : "+v"(m) : "v"(a), "v"(b));
+}
+
 struct View {
   float* p = nullptr;
   int B = 0, C = 0, T = 0, H = 0, W = 0;

@@ -84,15 +84,21 @@ __device__ __forceinline__ Tok token_of(int tk, const AttnGeom& g, long st, int 
 // probabilities and scaled q / k / v here are products, whose two fp16 roundings hipcc
 // would otherwise lower differently (hi + lo off by an fp16 ulp in ~2^-13 of the values;
 // it made the reciprocal-multiply softmax fail at 2.7e-4).
+// CHECK: OR |v| >= 65504 (fp16 overflow of hi) into bad; the probabilities (in [0, 1])
+// skip it. Plain C++ rather than the split2 asm (kernels.h): these splits read MFMA
+// results and feed MFMAs, and only compiler-visible VALU gets its MFMA hazard waits.
+template <bool CHECK = true>
 __device__ __forceinline__ void split8(const float* v, h8& hi, h8& lo, int& bad) {
+  float m = 0.f;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float w = split_src(v[e]);
-    bad |= fabsf(w) >= 65504.f;
+    if (CHECK) m = fmaxf(m, fabsf(w));
     const _Float16 a = (_Float16)w;
     hi[e] = a;
     lo[e] = (_Float16)(w - (float)a);
   }
+  if (CHECK) bad |= m >= 65504.f;
 }
 
 __device__ __forceinline__ f32x16 mma3(const h8& ah, const h8& al, const h8& bh, const h8& bl, f32x16 c) {
@@ -247,13 +253,18 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     for (int r = 0; r < 16; ++r) pacc[i][r] = 0.f;
 
   const float sq = wsc[0] * q_scale, sk = wsc[1], sv = wsc[2];
-  // RoPE factors of this lane's (token, dim pair) registers: the same for every unit
-  float rc[8], rs[8];
+  // RoPE factors of this lane's (token, dim pair) registers, the same for every unit (with
+  // the q / k scales folded in when FOLD)
+  // folded at C = 64 only: at C = 128 (one wave per SIMD) the 16 extra live registers
+  // cost 20 % (interleaved A/B)
+  constexpr bool FOLD = C == 64;
+  float rcq[8], rsq[8], rck[8], rsk[8];
 #pragma unroll
   for (int r = 0; r < 16; r += 2) {
     const int pi = (dof(r, h) % DH) >> 1;
-    rc[r >> 1] = rcos[me.rpos * RH + pi];
-    rs[r >> 1] = rsin[me.rpos * RH + pi];
+    const float c = rcos[me.rpos * RH + pi], sn = rsin[me.rpos * RH + pi];
+    rcq[r >> 1] = FOLD ? c * sq : c; rsq[r >> 1] = FOLD ? sn * sq : sn;
+    rck[r >> 1] = FOLD ? c * sk : c; rsk[r >> 1] = FOLD ? sn * sk : sn;
   }
   for (int u = 0; u < UNITS; ++u) {
     _Float16* W = wsm + (u & 1) * UL::HALVES;
@@ -282,13 +293,14 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     // scale, RoPE on (d, d+1) = registers (r, r+1); d = dof(r, h) within the head
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
-      const float c = rc[r >> 1], sn = rs[r >> 1];
-      const float q0 = q[r] * sq, q1 = q[r + 1] * sq;
-      q[r] = q0 * c + (-q1) * sn;
-      q[r + 1] = q1 * c + q0 * sn;
-      const float k0 = k[r] * sk, k1 = k[r + 1] * sk;
-      k[r] = k0 * c + (-k1) * sn;
-      k[r + 1] = k1 * c + k0 * sn;
+      float q0 = q[r], q1 = q[r + 1], k0 = k[r], k1 = k[r + 1];
+      if (!FOLD) {
+        q0 *= sq; q1 *= sq; k0 *= sk; k1 *= sk;
+      }
+      q[r] = q0 * rcq[r >> 1] - q1 * rsq[r >> 1];
+      q[r + 1] = q1 * rcq[r >> 1] + q0 * rsq[r >> 1];
+      k[r] = k0 * rck[r >> 1] - k1 * rsk[r >> 1];
+      k[r + 1] = k1 * rck[r >> 1] + k0 * rsk[r >> 1];
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] *= sv;
@@ -331,9 +343,14 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
         mx = fmaxf(mx, s_);
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32));
+      // exp(s - mx) as v_exp_f32 (2^x) of fma(s, log2 e, -mx log2 e): masked -inf -> 0
+      const float mxl = mx * 1.44269504088896341f;
       float sum = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { sc_[r] = expf(sc_[r] - mx); sum += sc_[r]; }
+      for (int r = 0; r < 16; ++r) {
+        sc_[r] = __builtin_amdgcn_exp2f(fmaf(sc_[r], 1.44269504088896341f, -mxl));
+        sum += sc_[r];
+      }
       sum += __shfl_xor(sum, 32);
       const float inv = 1.f / sum;
 #pragma unroll
@@ -346,7 +363,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 #pragma unroll
         for (int e = 0; e < 8; ++e) tp[e] = sc_[8 * s + e];
         h8 ph, pl;
-        split8(tp, ph, pl, bad);
+        split8<false>(tp, ph, pl, bad);
         h8 ah = vf[s][0], al = vf[s][1];
         if (!mine) {
 #pragma unroll
