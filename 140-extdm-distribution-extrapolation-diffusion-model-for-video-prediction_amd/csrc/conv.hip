@@ -12,6 +12,7 @@
 // MODE_DECONV runs ConvTranspose(1,4,4)/s2/p1 as four 2x2 parity convs
 // (blockIdx.z = parity); MODE_UP2 reads a nearest-x2-upsampled input.
 #include <cstdlib>
+#include <stdexcept>
 
 #include "kernels.h"
 
@@ -239,6 +240,7 @@ int conv_forward(hipStream_t s, const View& out, const View& in0, const View* in
   if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 &&
       conv_x3_forward(s, out, in0, in1, w, epi_in, &slots))
     return slots;
+  if (epi_in.res_aff) throw std::invalid_argument("conv: residual GroupNorm needs the f16x3 direct conv");
   ConvEpi epi = epi_in;  // the other paths leave the statistics to the caller
   epi.stats = nullptr;
   if (conv_gemm_x3_forward(s, out, in0, in1, w, stride, pad, epi)) return 0;

@@ -101,7 +101,11 @@ template <> struct XMaxX3<3, 512> { static constexpr int v = 800; };
 // is one contiguous run per plane, copied by LDS-DMA into the second X buffer during the
 // block's first stage as [hl][c8][pos][8]: no staging registers, loads, conversions or
 // LDS stores, and a lane's k-slice is 16 consecutive bytes (no swizzle needed).
-template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false>
+// RGN: the residual is GroupNorm + SiLU-normalised in the epilogue (ConvEpi::res_aff; 1x1
+// res_conv only — compiled out elsewhere: its live registers cost the 3x3 tiles their
+// second wave per SIMD).
+template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
+          bool RGN = false>
 __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   constexpr int NT = NW * 64;
   constexpr int PAD = KS / 2;
@@ -435,6 +439,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   // kernel-uniform branches only): per-element guarded loads made hipcc wait for each
   // one in turn, ~32 serial L2 round trips per wave at one workgroup per CU.
   const bool has_res = a.e.res != nullptr;
+  const bool res_gn = RGN && has_res;
   const bool has_post = a.e.post_scale != nullptr, post_pc = a.e.post_per_channel != 0;
   const int act = a.e.act;
   // GroupNorm statistics of the stored values, per 8-row block (i, k) of the lane's rows
@@ -483,6 +488,14 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
         for (int r16 = 0; r16 < 16; ++r16)
           rv[r16] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
               rs_res, (rbase + mrow[r16] * (int)a.e.res_sc) * 4, 0, 0));
+        if (res_gn) {  // the arithmetic of gn_apply_plane_kernel (norm.hip), no FiLM
+#pragma unroll
+          for (int r16 = 0; r16 < 16; ++r16) {
+            const float2 ab = a.e.res_aff[b * a.Cout + mrow[r16]];
+            const float w = rv[r16] * ab.x + ab.y;
+            rv[r16] = w / (1.f + expf(-w));
+          }
+        }
 #pragma unroll
         for (int r16 = 0; r16 < 16; ++r16) v[r16] += rv[r16];
       }
@@ -559,7 +572,8 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   }
 }
 
-template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false>
+template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
+          bool RGN = false>
 void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
   constexpr int AH = KY * NG * KS * (BM / 32) * 2 * 512;
   const size_t xlo = XOP ? (size_t)((a.XPOS + 63) & ~63) * 16 : (size_t)a.XPOS * NG * 16;
@@ -568,11 +582,11 @@ void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
   dim3 grid(ntiles, (a.Cout + BM - 1) / BM);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP>), grid, dim3(NW * 64), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN>), grid, dim3(NW * 64), lds, s, a);
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN>
@@ -686,6 +700,13 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   if (!x3_setup(out, in0, in1, w, epi, a, ntiles, stats_slots)) return false;
   const int ks = w.KH;
   const X3Tile tl{w.xbm, w.xbn, w.xng};
+  if (epi.res_aff) {  // residual GroupNorm: the 1x1 tiles only
+    if (ks != 1 || !epi.res || tl.bn != 128) return false;
+    if (tl.bm == 64) launch_sp<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, true>(s, a, ntiles);
+    else if (tl.bm == 128) launch_sp<1, 1, 128, 128, 2, 2, 4, 2, true, 1, false, true>(s, a, ntiles);
+    else return false;
+    return true;
+  }
   if (tl.bn == 512) {
     if (ks == 7 && tl.bm == 64) launch<7, 1, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
     else if (ks == 3 && tl.bm == 64) launch<3, 1, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
@@ -706,6 +727,17 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   else if (ks == 1 && tl.bm == 128) launch<1, 1, 128, 128, 2, 2, 4, 2>(s, a, ntiles);
   else return false;
   return true;
+}
+
+bool conv_x3_covers(const View& out, const View& in0, const View* in1, const PackedW& w) {
+  if (w.mode != MODE_CONV || w.KH != w.KW) return false;
+  X3Args a;
+  unsigned ntiles = 0;
+  const int ks = w.KH;
+  const bool tile_ok = (w.xbn == 512 && w.xbm == 64 && (ks == 7 || ks == 3)) ||
+                       (w.xbn != 512 && ((ks == 7 && w.xbm == 64) || (ks == 3 && (w.xbm == 64 || w.xbm == 128)) ||
+                                         (ks == 1 && (w.xbm == 64 || w.xbm == 128))));
+  return tile_ok && x3_setup(out, in0, in1, w, ConvEpi{}, a, ntiles, nullptr);
 }
 
 size_t x3op_halves(int B, int C, int T, int H, int W, int pad) {

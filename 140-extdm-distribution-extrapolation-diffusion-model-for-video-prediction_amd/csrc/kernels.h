@@ -105,6 +105,10 @@ struct ConvEpi {
   // kernel supports it): partials [b * stats_groups + g][slot][2] = (sum, sum of squares)
   double* stats = nullptr;
   int stats_groups = 0;
+  // GroupNorm + SiLU of the residual (conv_x3 1x1 only): r -> silu(r * a.x + a.y) with
+  // a = res_aff[b * Cout + c] = (rstd * gamma, beta - mean * rstd * gamma); the ResnetBlock's
+  // block2 norm folded into its res_conv (u12:199-203), so h2 is never normalised in place
+  const float2* res_aff = nullptr;
 };
 
 // Input channels per half-stage of the halo conv for kernel size ks and tile bm.
@@ -121,6 +125,8 @@ X3Tile x3_tile(int ks, int cout);
 // the epilogue wrote (0: not computed, the caller runs the statistics pass).
 bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                      const ConvEpi& epi, int* stats_slots = nullptr);
+// Whether conv_x3_forward covers this stride-1 'same' conv (no launch).
+bool conv_x3_covers(const View& out, const View& in0, const View* in1, const PackedW& w);
 // Pre-split f16x3 conv input ("operand") of an activation [B][C][T][H][W]: hi / lo fp16
 // halves as [hl][c8][C/16][B*T][H+2*pad][W+2*pad][8] with a zero ring of width pad:
 // channel 16*cg + 8*c8 + e of a padded position is element e of its 16-B record in
@@ -159,6 +165,11 @@ void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, c
 void groupnorm_silu_x3op(hipStream_t s, const View& x, const X3Op& out, int groups, const float* gamma,
                          const float* beta, const float* film, int film_row, int film_nt, const int* t_batch,
                          double* partials, int given_split = 0);
+// GroupNorm of x as a per-(b, c) affine table (rstd * gamma, beta - mean * rstd * gamma)
+// [B][C] (statistics pass unless given_split > 0), for a consumer that applies the norm
+// itself (ConvEpi::res_aff); stored in `partials` after the (mean, rstd) pairs
+const float2* groupnorm_affine(hipStream_t s, const View& x, int groups, const float* gamma, const float* beta,
+                               double* partials, int given_split = 0);
 
 // Channel LayerNorm (biased var over C, gamma only; u12:138-147) of in0 ++ in1.
 void channel_ln(hipStream_t s, const View& out, const View& in0, const View* in1, const float* gamma);

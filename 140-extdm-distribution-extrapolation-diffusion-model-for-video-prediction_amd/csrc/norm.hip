@@ -268,6 +268,19 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const double* __restric
   }
 }
 
+// (scale, shift) per (b, c) of a GroupNorm without FiLM: the per-element arithmetic of
+// gn_apply_plane_kernel is then w = v * scale + shift
+__global__ __launch_bounds__(256) void gn_affine_kernel(const float2* __restrict__ gst, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, int C, int Cg, int G,
+                                                        float2* __restrict__ tab) {
+  const int b = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const float2 mr = gst[b * G + c / Cg];
+    const float sc_ = mr.y * gamma[c];
+    tab[(long)b * C + c] = make_float2(sc_, beta[c] - mr.x * sc_);
+  }
+}
+
 // GroupNorm + FiLM + SiLU written as the pre-split f16x3 operand of the next 3x3 conv
 // (X3Op, kernels.h): one (sample b, 16-channel group cg) per grid.(y, z), one padded
 // position of the sample's T frames per thread (small planes share a workgroup); the
@@ -692,6 +705,14 @@ const float2* gn_mean_rstd(hipStream_t s, const View& x, int groups, double* par
 }
 
 }  // namespace
+
+const float2* groupnorm_affine(hipStream_t s, const View& x, int groups, const float* gamma, const float* beta,
+                               double* partials, int given_split) {
+  const float2* gst = gn_mean_rstd(s, x, groups, partials, given_split);
+  float2* tab = reinterpret_cast<float2*>(partials + (size_t)x.B * groups * 64 * 2 + (size_t)x.B * groups);
+  hipLaunchKernelGGL(gn_affine_kernel, dim3(x.B), dim3(256), 0, s, gst, gamma, beta, x.C, x.C / groups, groups, tab);
+  return tab;
+}
 
 void groupnorm_silu(hipStream_t s, const View& x, const View& out, int groups, const float* gamma,
                     const float* beta, const float* film, int film_row, int film_nt, const int* t_batch,

@@ -103,6 +103,8 @@ struct ExtdmHandle {
   double* partials = nullptr;
   // EXTDM_NO_GN_FUSE=1: separate GroupNorm statistics pass after every ResnetBlock conv
   const bool fuse_gn_stats = [] { const char* v = getenv("EXTDM_NO_GN_FUSE"); return !(v && v[0] && v[0] != '0'); }();
+  // EXTDM_NO_RES_GN=1: block2's GroupNorm applied in place before res_conv (A/B)
+  const bool fuse_res_gn = [] { const char* v = getenv("EXTDM_NO_RES_GN"); return !(v && v[0] && v[0] != '0'); }();
   int* t_batch = nullptr;
   int* step_ctr = nullptr;
   StepCoef* coefs = nullptr;
@@ -546,7 +548,16 @@ struct ExtdmHandle {
       h2 = alloc_cf(B, C, T, Hh, Ww);
       sp2 = conv(h2, h1, nullptr, w2, 1, 1, D(p + ".block2.proj.bias"), nullptr, ACT_NONE, nullptr, nullptr, 0, st, 8);
     }
-    if (has(p + ".res_conv.weight")) {
+    const PackedW* wr = has(p + ".res_conv.weight") ? &P(p + ".res_conv.weight") : nullptr;
+    if (wr && fuse_res_gn && x3_convs() && C <= 512 && wr->KH == 1 && wr->xbn == 128 && conv_x3_covers(out, in0, in1, *wr)) {
+      // block2's GroupNorm + SiLU applied to the residual inside res_conv's epilogue
+      if (plan) return;
+      ConvEpi e;
+      e.bias = D(p + ".res_conv.bias");
+      e.res = h2.p; e.res_sb = h2.sb; e.res_sc = h2.sc; e.res_st = h2.st;
+      e.res_aff = groupnorm_affine(s, h2, 8, D(p + ".block2.norm.weight"), D(p + ".block2.norm.bias"), partials, sp2);
+      REQUIRE(conv_x3_forward(s, out, in0, in1, *wr, e), "res_conv: f16x3 direct conv not covered");
+    } else if (wr) {
       if (!plan)
         groupnorm_silu(s, h2, h2, 8, D(p + ".block2.norm.weight"), D(p + ".block2.norm.bias"), nullptr, 0, 0,
                        nullptr, nullptr, partials, sp2);
@@ -1598,8 +1609,9 @@ struct ExtdmHandle {
     arena.top = 0;
     const size_t n = (size_t)3 * cfg.tp * cfg.latent * cfg.latent;
     eps_buf = dmalloc((size_t)B * n * sizeof(float));
-    // GroupNorm: [B][8 groups][64 slots][sum, sumsq], then (mean, rstd) per (b, group)
-    partials = reinterpret_cast<double*>(dmalloc(((size_t)B * 8 * 64 * 2 + (size_t)B * 8) * sizeof(double)));
+    // GroupNorm: [B][8 groups][64 slots][sum, sumsq], then (mean, rstd) per (b, group),
+    // then the [B][C <= 512] (scale, shift) table of groupnorm_affine
+    partials = reinterpret_cast<double*>(dmalloc(((size_t)B * 8 * 64 * 2 + (size_t)B * 8 + (size_t)B * 512) * sizeof(double)));
     t_batch = reinterpret_cast<int*>(dmalloc((size_t)std::max(B, 1) * sizeof(int)));
     step_ctr = reinterpret_cast<int*>(dmalloc(sizeof(int) * 4));
     HIPCHK(hipStreamCreateWithFlags(&work, hipStreamNonBlocking));

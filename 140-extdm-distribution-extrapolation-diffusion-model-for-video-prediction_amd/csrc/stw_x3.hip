@@ -172,7 +172,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   const Tok me = token_of<MODE>(lc, g, st, grp);
   int bad = 0;
   h8 xh[KS], xl[KS];
-  float m1 = 0.f, den1 = 1.f;
+  float m1 = 0.f, den1 = 1.f, rden1 = 1.f;
   {
     float xv[KS][8];
     float s = 0.f;
@@ -181,7 +181,8 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int c = 16 * k + 8 * h + e;
-        xv[k][e] = (active && me.valid) ? xb[(long)c * sc + me.pos] : 0.f;
+        // dbg & 4 (timing only): no x loads
+        xv[k][e] = (active && me.valid) ? ((dbg & 4) ? (float)(c ^ lane) * 0.01f : xb[(long)c * sc + me.pos]) : 0.f;
         s += xv[k][e];
       }
     s += __shfl_xor(s, 32);
@@ -193,13 +194,16 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       for (int e = 0; e < 8; ++e) { const float d = xv[k][e] - m1; v += d * d; }
     v += __shfl_xor(v, 32);
     den1 = sqrtf(v / C + 1e-5f);
+    // one reciprocal instead of a division per element (~10 VALU each, in the prologue and
+    // MODE 1's epilogue): the product differs from the quotient by at most an ulp
+    rden1 = 1.f / den1;
     if (MODE == 0) {
 #pragma unroll
       for (int k = 0; k < KS; ++k)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int c = 16 * k + 8 * h + e;
-          xv[k][e] = me.valid ? (xv[k][e] - m1) / den1 * gamma[c] : 0.f;
+          xv[k][e] = me.valid ? (xv[k][e] - m1) * rden1 * gamma[c] : 0.f;
         }
     } else {
       float s2 = 0.f;
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int c = 16 * k + 8 * h + e;
-          xv[k][e] = (xv[k][e] - m1) / den1 * gamma[c];
+          xv[k][e] = (xv[k][e] - m1) * rden1 * gamma[c];
           s2 += xv[k][e];
         }
       s2 += __shfl_xor(s2, 32);
@@ -389,6 +393,15 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   }
   if (bad) atomicOr(range_flag, 2);
   if (!active || !me.valid) return;
+  if (dbg & 8) {  // timing only: no epilogue loads / stores (one store keeps the work live)
+    float acc = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc += pacc[ct][r];
+    if (acc == 12345.f) ob[me.pos] = acc;
+    return;
+  }
 
   // ---- 3. bias + residual, write back ----
   const float spj = wsc[3];
@@ -401,7 +414,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       const float y = pacc[ct][r] * spj;
       float res;
       if (MODE == 0) res = (y + bp[c]) + xv;
-      else res = y + (xv + (xv - m1) / den1 * gamma[c]);
+      else res = y + (xv + (xv - m1) * rden1 * gamma[c]);
       ob[(long)c * osc + me.pos] = res;
     }
   }
