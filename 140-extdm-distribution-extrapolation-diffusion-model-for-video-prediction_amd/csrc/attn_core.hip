@@ -45,19 +45,20 @@ template <> struct Frag<false> {
 };
 template <> struct Frag<true> {
   h8 hi, lo;
-  // CHECK: OR |x| >= 65504 (fp16 overflow of hi) into bad; probabilities skip it. Plain
-  // C++ (not the split2 asm of kernels.h): the fragments feed MFMAs, and only
-  // compiler-visible VALU gets its MFMA hazard waits.
+  // CHECK: OR |x| >= 65504 (fp16 overflow of hi) into bad; probabilities skip it.
+  // Compiler-visible split2c, not the split2 asm of kernels.h: the fragments feed MFMAs,
+  // and only compiler-visible VALU gets its MFMA hazard waits.
   template <bool CHECK = true>
   __device__ void set(const float* x, int& bad) {
     float m = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float w = split_src(x[e]);
-      if (CHECK) m = fmaxf(m, fabsf(w));
-      const _Float16 a = (_Float16)w;
-      hi[e] = a;
-      lo[e] = (_Float16)(w - (float)a);
+    for (int e = 0; e < 8; e += 2) {  // split2c (kernels.h): 4 VALU per pair
+      const float w0 = split_src(x[e]), w1 = split_src(x[e + 1]);
+      if (CHECK) m = fmaxf(fmaxf(m, fabsf(w0)), fabsf(w1));
+      f16x2_t ph, pl;
+      split2c(w0, w1, ph, pl);
+      hi[e] = ph.x; hi[e + 1] = ph.y;
+      lo[e] = pl.x; lo[e + 1] = pl.y;
     }
     if (CHECK) bad |= m >= 65504.f;
   }

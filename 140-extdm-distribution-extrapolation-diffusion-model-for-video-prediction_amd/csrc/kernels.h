@@ -38,6 +38,20 @@ __device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned&
       : "=&v"(hi), "=v"(lo), "=&v"(da), "=&v"(db)
       : "v"(a), "v"(b));
 }
+// The same split in compiler-visible code (v_cvt_pk_f16_f32 of the pair, two v_fma_mix_f32
+// reading hi from the packed register, v_cvt_pk_f16_f32 of the remainders: 4 VALU per pair),
+// for values that come from or go to MFMAs: hipcc inserts the MFMA hazard waits itself.
+// hi is rounded once and lo reads that rounded register, so the two cannot disagree.
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split2c(float a, float b, f16x2_t& hi, f16x2_t& lo) {
+  hi = __builtin_convertvector((f32x2_t){a, b}, f16x2_t);
+  // an opaque 1.0: with a literal, instcombine turns the fma into fsub of a converted hi
+  const float one = split_src(1.0f);
+  const float la = __builtin_fmaf(-(float)hi.x, one, a);
+  const float lb = __builtin_fmaf(-(float)hi.y, one, b);
+  lo = __builtin_convertvector((f32x2_t){la, lb}, f16x2_t);
+}
 // m = max(m, |a|, |b|) in one v_max3_f32 (the fp16-range check of the split values;
 // the same hazard rule as split2)
 __device__ __forceinline__ void amax2(float& m, float a, float b) {

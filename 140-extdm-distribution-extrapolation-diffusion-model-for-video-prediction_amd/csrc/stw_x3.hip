@@ -85,18 +85,20 @@ __device__ __forceinline__ Tok token_of(int tk, const AttnGeom& g, long st, int 
 // would otherwise lower differently (hi + lo off by an fp16 ulp in ~2^-13 of the values;
 // it made the reciprocal-multiply softmax fail at 2.7e-4).
 // CHECK: OR |v| >= 65504 (fp16 overflow of hi) into bad; the probabilities (in [0, 1])
-// skip it. Plain C++ rather than the split2 asm (kernels.h): these splits read MFMA
-// results and feed MFMAs, and only compiler-visible VALU gets its MFMA hazard waits.
+// skip it. Compiler-visible split2c rather than the split2 asm (kernels.h): these splits
+// read MFMA results and feed MFMAs, and only compiler-visible VALU gets its MFMA hazard
+// waits (4 VALU per pair; the per-element cvt / cvt-back / sub / pack took 8).
 template <bool CHECK = true>
 __device__ __forceinline__ void split8(const float* v, h8& hi, h8& lo, int& bad) {
   float m = 0.f;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float w = split_src(v[e]);
-    if (CHECK) m = fmaxf(m, fabsf(w));
-    const _Float16 a = (_Float16)w;
-    hi[e] = a;
-    lo[e] = (_Float16)(w - (float)a);
+  for (int e = 0; e < 8; e += 2) {
+    const float w0 = split_src(v[e]), w1 = split_src(v[e + 1]);
+    if (CHECK) m = fmaxf(fmaxf(m, fabsf(w0)), fabsf(w1));
+    f16x2_t ph, pl;
+    split2c(w0, w1, ph, pl);
+    hi[e] = ph.x; hi[e + 1] = ph.y;
+    lo[e] = pl.x; lo[e + 1] = pl.y;
   }
   if (CHECK) bad |= m >= 65504.f;
 }
@@ -150,6 +152,22 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   const int grp = active ? gidx % groups_per_sample : 0;
   const float* xb = x + (long)b * sb;
   float* ob = out + (long)b * osb;
+  // Global traffic through buffer descriptors: a lane's 32-bit byte offset carries its token
+  // (and channel half), the channel row goes into the wave-uniform soffset, and an invalid
+  // token's offset lies past the extent (loads return 0, stores are dropped): no 64-bit
+  // address arithmetic and no divergent branch per element (the host checks the extents
+  // fit 31 bits).
+  constexpr int OOB = 0x40000000;
+  const int x_bytes = (int)(((long)(C - 1) * sc + (long)g.D * st) * 4);
+  const int o_bytes = (int)(((long)(C - 1) * osc + (long)g.D * st) * 4);
+  const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xb), 0, x_bytes, 0x00020000);
+  const auto rs_o = __builtin_amdgcn_make_buffer_rsrc(ob, 0, o_bytes, 0x00020000);
+  const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gamma), 0, C * 4, 0x00020000);
+  const auto rs_lw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(MODE == 1 ? ln_w : gamma), 0, C * 4, 0x00020000);
+  const auto rs_lb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(MODE == 1 ? ln_b : gamma), 0, C * 4, 0x00020000);
+  auto ldb = [](const __amdgpu_buffer_rsrc_t& r, int vo, int so) __attribute__((always_inline)) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+  };
 
   auto load_unit = [&](int u, _Float16* dst) {
     const _Float16* src = wpk + (long)u * UL::HALVES;
@@ -170,6 +188,8 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 
   // ---- 1. normalisation into register fragments ----
   const Tok me = token_of<MODE>(lc, g, st, grp);
+  const bool tok_ok = active && me.valid;
+  const int vpro = tok_ok ? (int)((8 * h * sc + me.pos) * 4) : OOB;  // channel 8h + (16k + e)
   int bad = 0;
   h8 xh[KS], xl[KS];
   float m1 = 0.f, den1 = 1.f, rden1 = 1.f;
@@ -182,7 +202,8 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       for (int e = 0; e < 8; ++e) {
         const int c = 16 * k + 8 * h + e;
         // dbg & 4 (timing only): no x loads
-        xv[k][e] = (active && me.valid) ? ((dbg & 4) ? (float)(c ^ lane) * 0.01f : xb[(long)c * sc + me.pos]) : 0.f;
+        xv[k][e] = (dbg & 4) ? (tok_ok ? (float)(c ^ lane) * 0.01f : 0.f)
+                             : ldb(rs_x, vpro, (int)((16 * k + e) * sc * 4));
         s += xv[k][e];
       }
     s += __shfl_xor(s, 32);
@@ -203,7 +224,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int c = 16 * k + 8 * h + e;
-          xv[k][e] = me.valid ? (xv[k][e] - m1) * rden1 * gamma[c] : 0.f;
+          xv[k][e] = me.valid ? (xv[k][e] - m1) * rden1 * ldb(rs_g, 32 * h, (16 * k + e) * 4) : 0.f;
         }
     } else {
       float s2 = 0.f;
@@ -212,7 +233,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int c = 16 * k + 8 * h + e;
-          xv[k][e] = (xv[k][e] - m1) * rden1 * gamma[c];
+          xv[k][e] = (xv[k][e] - m1) * rden1 * ldb(rs_g, 32 * h, (16 * k + e) * 4);
           s2 += xv[k][e];
         }
       s2 += __shfl_xor(s2, 32);
@@ -229,7 +250,9 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int c = 16 * k + 8 * h + e;
-          xv[k][e] = me.valid ? (xv[k][e] - m2) * rstd2 * ln_w[c] + ln_b[c] : 0.f;
+          xv[k][e] = me.valid ? (xv[k][e] - m2) * rstd2 * ldb(rs_lw, 32 * h, (16 * k + e) * 4) +
+                                    ldb(rs_lb, 32 * h, (16 * k + e) * 4)
+                              : 0.f;
         }
     }
 #pragma unroll
@@ -301,10 +324,11 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       if (!FOLD) {
         q0 *= sq; q1 *= sq; k0 *= sk; k1 *= sk;
       }
-      q[r] = q0 * rcq[r >> 1] - q1 * rsq[r >> 1];
-      q[r + 1] = q1 * rcq[r >> 1] + q0 * rsq[r >> 1];
-      k[r] = k0 * rck[r >> 1] - k1 * rsk[r >> 1];
-      k[r + 1] = k1 * rck[r >> 1] + k0 * rsk[r >> 1];
+      // one fma per output (a mul + fma instead of two muls and an add: one rounding fewer)
+      q[r] = fmaf(q0, rcq[r >> 1], -(q1 * rsq[r >> 1]));
+      q[r + 1] = fmaf(q1, rcq[r >> 1], q0 * rsq[r >> 1]);
+      k[r] = fmaf(k0, rck[r >> 1], -(k1 * rsk[r >> 1]));
+      k[r + 1] = fmaf(k1, rck[r >> 1], k0 * rsk[r >> 1]);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] *= sv;
@@ -404,18 +428,22 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   }
 
   // ---- 3. bias + residual, write back ----
+  // row c = cu + 4h of register r: the lane offset carries 4h, the soffset cu
   const float spj = wsc[3];
+  const int vex = (int)((4 * h * sc + me.pos) * 4), veo = (int)((4 * h * osc + me.pos) * 4);
+  const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(MODE == 0 ? bp : gamma), 0, C * 4, 0x00020000);
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int c = ct * 32 + dof(r, h);
-      const float xv = xb[(long)c * sc + me.pos];
+      const int cu = ct * 32 + (r & 3) + 8 * (r >> 2);
+      const float xv = ldb(rs_x, vex, (int)(cu * sc * 4));
+      const float pb = ldb(rs_b, 16 * h, cu * 4);  // MODE 0: proj bias; MODE 1: gamma
       const float y = pacc[ct][r] * spj;
       float res;
-      if (MODE == 0) res = (y + bp[c]) + xv;
-      else res = y + (xv + (xv - m1) * rden1 * gamma[c]);
-      ob[(long)c * osc + me.pos] = res;
+      if (MODE == 0) res = (y + pb) + xv;
+      else res = y + (xv + (xv - m1) * rden1 * pb);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(res), rs_o, veo, (int)(cu * osc * 4), 0);
     }
   }
 }
@@ -473,11 +501,16 @@ bool attn_x3_supported(int C, int ntok, int dim_head, int heads) {
   return heads == 8 && (C == 64 || C == 128) && ntok <= 32 && (dim_head == 32 || dim_head == 16);
 }
 
+// the kernels address a sample of x / out with 31-bit byte offsets (buffer descriptors)
+static bool extent_ok(const View& v, const AttnGeom& g) {
+  return ((long)(v.C - 1) * v.sc + (long)g.D * v.st) * 4 < (1L << 30) && v.st == (long)v.H * v.W;
+}
+
 bool stw_x3(hipStream_t s, const View& x, const AttnGeom& g, int heads, int dim_head, const float* gamma,
             const void* wpk, const float* wsc, const float* bp, const float* bias_dense, int bstride,
             const float* rcos, const float* rsin, float q_scale) {
   const int N = g.ws0 * g.ws1 * g.ws2;
-  if (!attn_x3_supported(x.C, N, dim_head, heads)) return false;
+  if (!attn_x3_supported(x.C, N, dim_head, heads) || !extent_ok(x, g)) return false;
   const int groups = (g.Dp / g.ws0) * (g.Hp / g.ws1) * (g.Wp / g.ws2);
   if (dim_head == 32)
     return dispatch_c<0, 32>(s, x, x, g, groups, gamma, nullptr, nullptr, wpk, wsc, bp, bias_dense, bstride, rcos,
@@ -489,7 +522,7 @@ bool stw_x3(hipStream_t s, const View& x, const AttnGeom& g, int heads, int dim_
 bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, int dim_head,
                  const float* gamma, const float* ln_w, const float* ln_b, const void* wpk, const float* wsc,
                  const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale) {
-  if (!attn_x3_supported(x.C, g.D, dim_head, heads) || g.D > 32) return false;
+  if (!attn_x3_supported(x.C, g.D, dim_head, heads) || g.D > 32 || !extent_ok(x, g) || !extent_ok(out, g)) return false;
   if (out.sc != x.sc || out.st != x.st) return false;
   const int ppb = g.D <= 16 ? 2 : 1;
   const int groups = (g.H * g.W + ppb - 1) / ppb;
