@@ -21,6 +21,7 @@
 // The unit's packed weights (q, k, v, proj slices; hi/lo fp16, pre-scaled by a power
 // of two per matrix) are shared by the block's waves through a double-buffered
 // LDS-DMA ring, one barrier per unit.
+#include <algorithm>
 #include <cstdlib>
 
 #include "kernels.h"
@@ -416,6 +417,43 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     }
   }
   if (bad) atomicOr(range_flag, 2);
+  // MODE 1 with 2-pixel groups: a lane's token is (pixel, frame), so a direct store touches
+  // 16 frame planes per instruction, 8 bytes each, and every 64-B line is written by 8
+  // waves. Instead the workgroup's 16 consecutive pixels x D frames x C channels go through
+  // LDS ([c][t][16 px], rows padded for conflict-free lane writes) and leave as 64-B rows.
+  const bool lds_epi = MODE == 1 && C == 64 && NW == 8 && g.D <= 16 && groups_per_sample % NW == 0 && (g.H * g.W) % 16 == 0 &&
+                       (osc & 3) == 0 && (st & 3) == 0 && (((uintptr_t)out) & 15) == 0;
+  if (MODE == 1 && lds_epi) {
+    constexpr int RS = 20, CS = 16 * RS + 8;  // CS % 16 == 8: the two lane halves hit other banks
+    float* T = reinterpret_cast<float*>(wsm);
+    __syncthreads();  // every wave is done with the weight ring
+    const int pl = wave * 2 + (lc >> 4), tt = lc & 15;
+    const float spj = wsc[3];
+    const int vex = (int)((4 * h * sc + me.pos) * 4);
+    if (active) {
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int cu = ct * 32 + (r & 3) + 8 * (r >> 2);
+          const float xv = ldb(rs_x, vex, (int)(cu * sc * 4));
+          const float y = pacc[ct][r] * spj;
+          const float res = y + (xv + (xv - m1) * rden1 * ldb(rs_g, 16 * h, cu * 4));
+          T[(cu + 4 * h) * CS + tt * RS + pl] = res;
+        }
+    }
+    __syncthreads();
+    if (!active) return;
+    const int hw0 = (blockIdx.x * NW) % groups_per_sample * 2;
+    float* o0 = ob + hw0;
+    for (int i = tid; i < C * g.D * 4; i += NW * 64) {
+      const int q = i & 3, ctr = i >> 2;
+      const int t = ctr % g.D, c = ctr / g.D;
+      const float4 v = *reinterpret_cast<const float4*>(T + c * CS + t * RS + 4 * q);
+      *reinterpret_cast<float4*>(o0 + (long)c * osc + (long)t * st + 4 * q) = v;
+    }
+    return;
+  }
   if (!active || !me.valid) return;
   if (dbg & 8) {  // timing only: no epilogue loads / stores (one store keeps the work live)
     float acc = 0.f;
@@ -453,7 +491,10 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
                const float* lw, const float* lb, const void* wpk, const float* wsc, const float* bp,
                const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale) {
   static const int dbg = [] { const char* v = getenv("EXTDM_X3_DBG"); return v ? atoi(v) : 0; }();
-  const size_t lds = (size_t)2 * UnitLayout<C>::HALVES * sizeof(_Float16);
+  // MODE 1 at C = 64, 8 waves: the epilogue's [C][16 frames][16 px] staging tile (rows of
+  // 20, channels of 328 floats) reuses the ring
+  const size_t ring = (size_t)2 * UnitLayout<C>::HALVES * sizeof(_Float16);
+  const size_t lds = (MODE == 1 && C == 64 && NW == 8) ? std::max(ring, (size_t)C * 328 * sizeof(float)) : ring;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW>),
