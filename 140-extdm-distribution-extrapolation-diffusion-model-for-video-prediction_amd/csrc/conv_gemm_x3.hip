@@ -36,6 +36,7 @@ struct GArgs {
   ConvEpi e;
   long N;
   int* range;
+  int in_bytes;  // FAST: byte extent of in0 (the buffer descriptor's range; < 2^30)
 };
 
 __device__ __forceinline__ float act_apply(float v, int act) {
@@ -48,7 +49,13 @@ __device__ __forceinline__ float act_apply(float v, int act) {
   }
 }
 
-template <int KH, int KW, int BM, int MODE>
+// FAST (KH * KW divides 32, no nearest-up, one source; the host checks the byte extents fit
+// 31 bits): a thread's 16 gather elements per K tile have the same taps (ky, kx) in every
+// tile -- the tile's channels are the only change, and they are wave-uniform -- so the
+// element's in-image test and its byte offset are computed once, and each load is a buffer
+// load with that offset (an invalid tap's offset lies past the extent: the load returns 0)
+// and the tile's channel offset in soffset: no per-element address math or branch.
+template <int KH, int KW, int BM, int MODE, bool FAST = false>
 __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
   constexpr int WAVES_M = BM >= 64 ? 2 : 1;
   constexpr int WAVES_N = 4 / WAVES_M;
@@ -106,10 +113,45 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
   const int K = a.Cin * KK;
 
   float breg[2][8];
-  uint4 areg[APASS];
+  u32x4 areg[APASS];  // ext_vector (HIP's uint4 struct kept the array in scratch)
   int bad = 0;
 
-  auto load_tile = [&](int kt) {
+  static_assert(!FAST || (BK % KK == 0 && MODE != MODE_UP2), "FAST: taps repeat per K tile");
+  constexpr int CPT = BK / KK;  // channels per K tile (FAST)
+  constexpr int OOB = 0x40000000;
+  int voff[2][8];
+  // the range is the tensor's extent: an invalid tap's offset (OOB) lies past it and reads 0
+  const auto rs_in = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in0), 0, a.in_bytes, 0x00020000);
+  if (FAST) {
+#pragma unroll
+    for (int g2 = 0; g2 < 2; ++g2)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int kl = 8 * (kg + 2 * g2) + e;  // wave-uniform
+        const int tap = kl % KK;
+        const int iy = iy0 + tap / KW, ix = ix0 + tap % KW;
+        const bool ok = nvalid && iy >= 0 && iy < Hv && ix >= 0 && ix < Wv;
+        voff[g2][e] = ok ? (int)((base0 + (long)iy * a.Win + ix) * 4) : OOB;
+      }
+  }
+
+  auto load_tile = [&](int kt) __attribute__((always_inline)) {
+    if (FAST) {
+#pragma unroll
+      for (int g2 = 0; g2 < 2; ++g2)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int ci = __builtin_amdgcn_readfirstlane(kt * CPT + (8 * (kg + 2 * g2) + e) / KK);
+          const int cl = ci < a.Cin ? ci : a.Cin - 1;  // the K tail reads a real channel, zeroed
+          const float v = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(rs_in, voff[g2][e], (int)(cl * a.i0c * 4), 0));
+          breg[g2][e] = ci < a.Cin ? v : 0.f;
+        }
+      const u32x4* ap = reinterpret_cast<const u32x4*>(wbase + (long)kt * AH);
+#pragma unroll
+      for (int p = 0; p < APASS; ++p) areg[p] = ap[p * 256 + tid];
+      return;
+    }
 #pragma unroll
     for (int g2 = 0; g2 < 2; ++g2) {
 #pragma unroll
@@ -131,11 +173,11 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
         breg[g2][e] = v;
       }
     }
-    const uint4* ap = reinterpret_cast<const uint4*>(wbase + (long)kt * AH);
+    const u32x4* ap = reinterpret_cast<const u32x4*>(wbase + (long)kt * AH);
 #pragma unroll
     for (int p = 0; p < APASS; ++p) areg[p] = ap[p * 256 + tid];
   };
-  auto store_tile = [&](_Float16* As, _Float16* Bs) {
+  auto store_tile = [&](_Float16* As, _Float16* Bs) __attribute__((always_inline)) {
 #pragma unroll
     for (int g2 = 0; g2 < 2; ++g2) {
       const int g = kg + 2 * g2;  // 8-k group: step g >> 1, half g & 1
@@ -153,7 +195,7 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
       *reinterpret_cast<h8*>(d) = hi;
       *reinterpret_cast<h8*>(d + 2 * BN * 16) = lo;
     }
-    uint4* ad = reinterpret_cast<uint4*>(As);
+    u32x4* ad = reinterpret_cast<u32x4*>(As);
 #pragma unroll
     for (int p = 0; p < APASS; ++p) ad[p * 256 + tid] = areg[p];
   };
@@ -172,7 +214,9 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
   for (int kt = 0; kt < a.nkt; ++kt) {
     const _Float16* As = (kt & 1) ? As1 : As0;
     const _Float16* Bs = (kt & 1) ? Bs1 : Bs0;
-    if (kt + 1 < a.nkt) load_tile(kt + 1);
+    // unconditional prefetch (the last tile re-loads itself into the idle buffer): under a
+    // condition hipcc kept the A prefetch registers in scratch
+    load_tile(kt + 1 < a.nkt ? kt + 1 : kt);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       h8 ah[TM], al[TM], bh[TN], bl[TN];
@@ -198,7 +242,7 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
     }
-    if (kt + 1 < a.nkt) store_tile((kt & 1) ? As0 : As1, (kt & 1) ? Bs0 : Bs1);
+    store_tile((kt & 1) ? As0 : As1, (kt & 1) ? Bs0 : Bs1);
     __syncthreads();
   }
   if (bad) atomicOr(a.range, 1);
@@ -238,17 +282,43 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
   }
 }
 
-template <int KH, int KW, int BM, int MODE>
-void launch(hipStream_t s, const GArgs& a, dim3 grid) {
+template <int KH, int KW, int BM, int MODE, bool FAST>
+void launch_f(hipStream_t s, const GArgs& a, dim3 grid) {
   constexpr int AH = 2 * (BM / 32) * 2 * 512, BH = 2 * 2 * BN * 16;
   const size_t lds = (size_t)2 * (AH + BH) * sizeof(_Float16);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_x3_kernel<KH, KW, BM, MODE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_x3_kernel<KH, KW, BM, MODE, FAST>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_gemm_x3_kernel<KH, KW, BM, MODE>), grid, dim3(256), lds, s, a);
+  hipLaunchKernelGGL((conv_gemm_x3_kernel<KH, KW, BM, MODE, FAST>), grid, dim3(256), lds, s, a);
+}
+
+// the fast gather (FAST above): taps that repeat per K tile, one source, 31-bit byte offsets
+bool gemm_fast_ok(const GArgs& a, int kk, int mode) {
+  static const bool off = [] { const char* v = getenv("EXTDM_GEMM_NOFAST"); return v && v[0] && v[0] != '0'; }();
+  if (off || BK % kk != 0 || mode == MODE_UP2 || a.Cin != a.C0) return false;
+  const long bytes = ((long)(a.B - 1) * a.i0b + (long)(a.Cin - 1) * a.i0c + (long)(a.T - 1) * a.i0t +
+                      (long)a.Hin * a.Win) * 4;
+  return bytes < (1L << 30);
+}
+int gemm_in_bytes(const GArgs& a) {
+  return (int)(((long)(a.B - 1) * a.i0b + (long)(a.Cin - 1) * a.i0c + (long)(a.T - 1) * a.i0t +
+                (long)a.Hin * a.Win) * 4);
+}
+
+template <int KH, int KW, int BM, int MODE>
+void launch(hipStream_t s, const GArgs& a, dim3 grid) {
+  if constexpr (BK % (KH * KW) == 0 && MODE != MODE_UP2) {
+    if (gemm_fast_ok(a, KH * KW, MODE)) {
+      GArgs f = a;
+      f.in_bytes = gemm_in_bytes(a);
+      launch_f<KH, KW, BM, MODE, true>(s, f, grid);
+      return;
+    }
+  }
+  launch_f<KH, KW, BM, MODE, false>(s, a, grid);
 }
 
 template <int KH, int KW, int MODE>
