@@ -49,6 +49,8 @@ struct X3Args {
   int stats_split;           // GroupNorm partial slots per (b, group) when e.stats is set
   // XOP: pre-split input operand (X3Op, kernels.h) copied by LDS-DMA instead of staged
   const _Float16* xop; long xop_cg, xop_hl;  // halves per channel group / per hi|lo half
+  // split-K (SPL): fp32 partial accumulators [z][mtile][tile][TM*TN*16][NT], nsplit slices
+  float* part; int nsplit;
   ConvEpi e;
 };
 
@@ -104,8 +106,12 @@ template <> struct XMaxX3<3, 512> { static constexpr int v = 800; };
 // RGN: the residual is GroupNorm + SiLU-normalised in the epilogue (ConvEpi::res_aff; 1x1
 // res_conv only — compiled out elsewhere: its live registers cost the 3x3 tiles their
 // second wave per SIMD).
+// SPL: split-K for launches with few workgroups (the small levels' long K loops were bound
+// by the per-stage weight stream of too few CUs): 1 = slice blockIdx.z of the channel
+// blocks, accumulators stored as fp32 partials; 2 = the partials summed in slice order
+// (deterministic) and the normal epilogue.
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
-          bool RGN = false>
+          bool RGN = false, int SPL = 0>
 __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   constexpr int NT = NW * 64;
   constexpr int PAD = KS / 2;
@@ -144,7 +150,9 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   const int THK = a.TH + KS - 1;
   // first halo position of the tile in the operand's padded [P][H+KS-1][RS] planes
   const int tb = (plane0 * (a.H + KS - 1) + row0) * a.RS;
-  const int NIT = a.ncgb * STG;
+  const int c0 = SPL == 1 ? (int)blockIdx.z * a.ncgb / a.nsplit : 0;
+  const int c1 = SPL == 1 ? ((int)blockIdx.z + 1) * a.ncgb / a.nsplit : a.ncgb;
+  const int NIT = c1 * STG;
   const _Float16* wt = a.w + (long)mtile * a.ncgb * KS * AH;
 
   // ---- staging slots: (group, halo position), 16 channels each ----
@@ -337,15 +345,29 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
     ep_sc[tid] = a.wscale[mc];
     ep_bi[tid] = a.e.bias ? a.e.bias[mc] : 0.f;
   }
-  if (XOP) {
-    dma_x(0, Xs0);
-    load_a(0, As0);
+  if (SPL == 2) {
+    // sum of the slices' partial accumulators, in slice order
+    const long per = (long)TM * TN * 16 * NT;
+    const float* pp = a.part + ((long)mtile * gridDim.x + tile) * per + tid;
+    const long zs = (long)gridDim.y * gridDim.x * per;
+    for (int z = 0; z < a.nsplit; ++z)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] += pp[z * zs + (long)((i * TN + j) * 16 + r) * NT];
+    __syncthreads();  // ep_sc / ep_bi
+  } else if (XOP) {
+    dma_x(c0, Xs0);
+    load_a(c0 * STG, As0);
   } else {
-    load_x(0);
-    load_a(0, As0);
-    store_x(Xs0, 0);
+    load_x(c0);
+    load_a(c0 * STG, As0);
+    store_x(Xs0, c0);
   }
-  if (SPAN) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the asm DMA is invisible to __syncthreads
+  if (SPL == 2) {
+  } else if (SPAN) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the asm DMA is invisible to __syncthreads
   else __syncthreads();
   // One (channel block, ky block) stage. `more` = a next channel block exists (its X is
   // prefetched at stage 0 and stored at stage STG - 1). The stages of a channel block are
@@ -355,13 +377,14 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   // wait vmcnt(0) before re-loading the xr registers, right behind the stage's A DMA).
   auto stage = [&](int cgb, int kb, bool more) __attribute__((always_inline)) {
     const int it = cgb * STG + kb;
-    const _Float16* Ast = (it & 1) ? As1 : As0;
-    const _Float16* Xs = (cgb & 1) ? Xs1 : Xs0;
-    if (it + 1 < NIT) load_a(it + 1, (it & 1) ? As0 : As1);
+    const int itr = it - c0 * STG, cr = cgb - c0;  // ring / buffer parity from the slice start
+    const _Float16* Ast = (itr & 1) ? As1 : As0;
+    const _Float16* Xs = (cr & 1) ? Xs1 : Xs0;
+    if (it + 1 < NIT) load_a(it + 1, (itr & 1) ? As0 : As1);
     const bool pre = (kb == 0) && more;
     if (SPAN) __builtin_amdgcn_sched_barrier(0);  // the X loads issue after the DMA (vmcnt order)
     if (pre) {
-      if (XOP) dma_x(cgb + 1, (cgb & 1) ? Xs0 : Xs1);
+      if (XOP) dma_x(cgb + 1, (cr & 1) ? Xs0 : Xs1);
       else load_x(cgb + 1);
     }
 #pragma unroll
@@ -404,7 +427,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
         if (SPAN) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         else __syncthreads();
       }
-      store_x((cgb & 1) ? Xs0 : Xs1, cgb + 1);
+      store_x((cr & 1) ? Xs0 : Xs1, cgb + 1);
     }
     if (SPAN) {
       // retire this stage's A DMA (issued before the X prefetch) and this wave's LDS
@@ -430,9 +453,22 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
       for (int kb = 1; kb < STG; ++kb) stage(cgb, kb, more);
     }
   };
-  for (int cgb = 0; cgb + 1 < a.ncgb; ++cgb) channel_block(cgb, true);
-  channel_block(a.ncgb - 1, false);
+  if (SPL != 2) {
+    for (int cgb = c0; cgb + 1 < c1; ++cgb) channel_block(cgb, true);
+    channel_block(c1 - 1, false);
+  }
   if (range_bad) atomicOr(&g_x3_range, 1);
+  if (SPL == 1) {
+    const long per = (long)TM * TN * 16 * NT;
+    float* pp = a.part + (((long)blockIdx.z * gridDim.y + mtile) * gridDim.x + tile) * per + tid;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) pp[(long)((i * TN + j) * 16 + r) * NT] = acc[i][j][r];
+    return;
+  }
 
   // ---- epilogue (C/D map: col = lane & 31, row = (r&3) + 8(r>>2) + 4h) ----
   // Every operand load of a row group is issued before its first use (clamped indices,
@@ -573,20 +609,20 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
-          bool RGN = false>
+          bool RGN = false, int SPL = 0>
 void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
   constexpr int AH = KY * NG * KS * (BM / 32) * 2 * 512;
   const size_t xlo = XOP ? (size_t)((a.XPOS + 63) & ~63) * 16 : (size_t)a.XPOS * NG * 16;
   // + 32 halves (unused-slot dummy) + 2 * BM floats (epilogue scale / bias)
   const size_t lds = ((size_t)2 * AH + (size_t)XBUF * 2 * xlo + 32 + 4 * BM) * sizeof(_Float16);
-  dim3 grid(ntiles, (a.Cout + BM - 1) / BM);
+  dim3 grid(ntiles, (a.Cout + BM - 1) / BM, SPL == 1 ? a.nsplit : 1);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN>), grid, dim3(NW * 64), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL>), grid, dim3(NW * 64), lds, s, a);
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN>
@@ -604,6 +640,24 @@ void launch_ns(hipStream_t s, const X3Args& a, unsigned ntiles) {
     else if (need == 2) launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 2>(s, a, ntiles);
     else launch_sp<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, 3>(s, a, ntiles);
   }
+}
+
+// Split-K for launches that leave CUs idle: the 3x3 128-row tile runs one workgroup per CU
+// (84 KB of LDS), so it splits only below 128 workgroups and up to 256 in total (a second
+// round of workgroups cost more than the shorter K loops saved: 70 -> 80 us at 256 x 2);
+// the 1x1 128-row tile (several workgroups per CU) splits below 384, up to 512. Slices keep
+// >= 2 channel blocks, and the partials (S x workgroups x tile floats) must fit the
+// workspace. EXTDM_NO_SPLITK=1 turns it off (A/B).
+bool split_k(X3Args& a, unsigned ntiles, int tile_elems, const ConvEpi& e, long max_wg, long max_total) {
+  static const bool off = [] { const char* v = getenv("EXTDM_NO_SPLITK"); return v && v[0] && v[0] != '0'; }();
+  const long nwg = (long)ntiles * ((a.Cout + 127) / 128);
+  if (off || !e.split_ws || nwg >= max_wg || a.ncgb < 4) return false;
+  int S = (int)std::min<long>(a.ncgb / 2, max_total / nwg);
+  while (S >= 2 && (size_t)S * nwg * tile_elems * sizeof(float) > e.split_ws_bytes) --S;
+  if (S < 2) return false;
+  a.part = e.split_ws;
+  a.nsplit = S;
+  return true;
 }
 
 int x3_v3() {
@@ -624,7 +678,12 @@ void launch(hipStream_t s, const X3Args& a, unsigned ntiles) {
 X3Tile x3_tile(int ks, int cout) {
   X3Tile t{};
   // 7x7 (init_conv): 16 waves over 64 x 512 px tiles, one X buffer; 3x3: 8 waves
-  if (ks == 7) { t.bm = 64; t.bn = 512; t.ng = 1; }
+  if (ks == 7) {
+    // EXTDM_X3_BN7=256: the 8-wave 64 x 256 tile (two X buffers, no spills) instead of the
+    // 16-wave 64 x 512 one (148 B of scratch per lane outside the MFMA loop)
+    static const int bn7 = [] { const char* v = getenv("EXTDM_X3_BN7"); return v ? atoi(v) : 512; }();
+    t.bm = 64; t.bn = bn7 == 256 ? 256 : 512; t.ng = 1;
+  }
   else if (ks == 3) {
     // EXTDM_X3_BN3: pixel tile of the Cout <= 64 3x3 convs (256 or 512)
     static const int bn3 = [] { const char* v = getenv("EXTDM_X3_BN3"); return v ? atoi(v) : 256; }();
@@ -722,9 +781,23 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     if (x3_v3() == 1) launch<3, 3, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
     else launch<3, 1, 64, 256, 1, 4, 4, 2>(s, a, ntiles);
   }
-  else if (ks == 3 && tl.bm == 128) launch<3, 1, 128, 128, 1, 2, 8, 2>(s, a, ntiles);
+  else if (ks == 3 && tl.bm == 128) {
+    if (split_k(a, ntiles, 128 * 128, epi, 128, 256)) {
+      launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, false, false, 1>(s, a, ntiles);
+      launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, false, false, 2>(s, a, ntiles);
+    } else {
+      launch<3, 1, 128, 128, 1, 2, 8, 2>(s, a, ntiles);
+    }
+  }
   else if (ks == 1 && tl.bm == 64) launch<1, 1, 64, 128, 2, 4, 4, 2>(s, a, ntiles);
-  else if (ks == 1 && tl.bm == 128) launch<1, 1, 128, 128, 2, 2, 4, 2>(s, a, ntiles);
+  else if (ks == 1 && tl.bm == 128) {
+    if (split_k(a, ntiles, 128 * 128, epi, 384, 512)) {
+      launch_sp<1, 1, 128, 128, 2, 2, 4, 2, true, 1, false, false, 1>(s, a, ntiles);
+      launch_sp<1, 1, 128, 128, 2, 2, 4, 2, true, 1, false, false, 2>(s, a, ntiles);
+    } else {
+      launch<1, 1, 128, 128, 2, 2, 4, 2>(s, a, ntiles);
+    }
+  }
   else return false;
   return true;
 }
@@ -781,6 +854,9 @@ bool conv_x3_forward_op(hipStream_t s, const View& out, const X3Op& in, const Pa
   if (w.xbm == 64) {
     if (x3_v3() == 1) launch_sp<3, 3, 64, 256, 1, 4, 8, 2, true, 1, true>(s, a, ntiles);
     else launch_sp<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true>(s, a, ntiles);
+  } else if (split_k(a, ntiles, 128 * 128, epi, 128, 256)) {
+    launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true, false, 1>(s, a, ntiles);
+    launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true, false, 2>(s, a, ntiles);
   } else {
     launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true>(s, a, ntiles);
   }

@@ -123,6 +123,10 @@ struct ConvEpi {
   // a = res_aff[b * Cout + c] = (rstd * gamma, beta - mean * rstd * gamma); the ResnetBlock's
   // block2 norm folded into its res_conv (u12:199-203), so h2 is never normalised in place
   const float2* res_aff = nullptr;
+  // split-K workspace (conv_x3, launches of few workgroups): fp32 partials, reused by every
+  // conv of the stream in turn
+  float* split_ws = nullptr;
+  size_t split_ws_bytes = 0;
 };
 
 // Input channels per half-stage of the halo conv for kernel size ks and tile bm.

@@ -101,6 +101,9 @@ struct ExtdmHandle {
   // workspace
   Arena arena;
   double* partials = nullptr;
+  // split-K partials of the direct convs (ConvEpi::split_ws): 512 workgroups x 128 x 128 fp32
+  float* split_ws = nullptr;
+  static constexpr size_t kSplitWsBytes = (size_t)512 * 128 * 128 * sizeof(float);
   // EXTDM_NO_GN_FUSE=1: separate GroupNorm statistics pass after every ResnetBlock conv
   const bool fuse_gn_stats = [] { const char* v = getenv("EXTDM_NO_GN_FUSE"); return !(v && v[0] && v[0] != '0'); }();
   // EXTDM_NO_RES_GN=1: block2's GroupNorm applied in place before res_conv (A/B)
@@ -507,6 +510,8 @@ struct ExtdmHandle {
     e.post_scale = ps;
     e.post_shift = psh;
     e.post_per_channel = per_channel;
+    e.split_ws = split_ws;
+    e.split_ws_bytes = split_ws ? kSplitWsBytes : 0;
     return conv_forward(s, out, in0, in1, w, stride, pad, e);
   }
 
@@ -539,6 +544,8 @@ struct ExtdmHandle {
         e.bias = D(p + ".block2.proj.bias");
         e.stats = st;
         e.stats_groups = 8;
+        e.split_ws = split_ws;
+        e.split_ws_bytes = split_ws ? kSplitWsBytes : 0;
         REQUIRE(conv_x3_forward_op(s, h2, op, w2, e, &sp2), "block2 conv: operand input not covered");
       }
     } else {
@@ -555,6 +562,8 @@ struct ExtdmHandle {
       ConvEpi e;
       e.bias = D(p + ".res_conv.bias");
       e.res = h2.p; e.res_sb = h2.sb; e.res_sc = h2.sc; e.res_st = h2.st;
+      e.split_ws = split_ws;
+      e.split_ws_bytes = split_ws ? kSplitWsBytes : 0;
       e.res_aff = groupnorm_affine(s, h2, 8, D(p + ".block2.norm.weight"), D(p + ".block2.norm.bias"), partials, sp2);
       REQUIRE(conv_x3_forward(s, out, in0, in1, *wr, e), "res_conv: f16x3 direct conv not covered");
     } else if (wr) {
@@ -1611,6 +1620,7 @@ struct ExtdmHandle {
     eps_buf = dmalloc((size_t)B * n * sizeof(float));
     // GroupNorm: [B][8 groups][64 slots][sum, sumsq], then (mean, rstd) per (b, group),
     // then the [B][C <= 512] (scale, shift) table of groupnorm_affine
+    split_ws = reinterpret_cast<float*>(dmalloc(kSplitWsBytes));
     partials = reinterpret_cast<double*>(dmalloc(((size_t)B * 8 * 64 * 2 + (size_t)B * 8 + (size_t)B * 512) * sizeof(double)));
     t_batch = reinterpret_cast<int*>(dmalloc((size_t)std::max(B, 1) * sizeof(int)));
     step_ctr = reinterpret_cast<int*>(dmalloc(sizeof(int) * 4));
