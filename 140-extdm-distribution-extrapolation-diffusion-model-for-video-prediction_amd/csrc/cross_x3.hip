@@ -192,7 +192,167 @@ __global__ __launch_bounds__(256) void cross_attn_x3_kernel(const float* __restr
   }
 }
 
+// ---- pre-split K / V (the cond cache: k and v depend on the cond frames only) ----
+// kvp[b][head][key tile kt][k | v][s][hl][64 lanes][8]: the MFMA A fragments of one
+// 32-key tile, split once per sampling call exactly as the staged kernel splits them:
+//   K (S^T = K·Q^T): lane (h, lc) element e = K[dim 16s + 8h + e][key 32kt + lc];
+//   V (O^T = V^T·P^T): lane (h, lc) element e = V[dim lc][key 32kt + 16s + 8(e>>2) + 4h + (e&3)]
+// (keys >= NK are zero; their scores are masked).
+__global__ __launch_bounds__(256) void cross_kv_split_kernel(const float* __restrict__ K, const float* __restrict__ V,
+                                                             _Float16* __restrict__ kvp, int C, int heads, int NK,
+                                                             int nkt, long total, int* __restrict__ range) {
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;  // (b, head, kt, kv, s, lane)
+  if (gid >= total) return;
+  const int lane = (int)(gid & 63);
+  long r = gid >> 6;
+  const int s = (int)(r & 1); r >>= 1;
+  const int kv = (int)(r & 1); r >>= 1;
+  const int kt = (int)(r % nkt); r /= nkt;
+  const int hd = (int)(r % heads);
+  const int b = (int)(r / heads);
+  const int h = lane >> 5, lc = lane & 31;
+  const float* src = (kv ? V : K) + ((long)b * C + hd * 32) * NK;
+  h8 hi, lo;
+  int bad = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int dim = kv ? lc : 16 * s + 8 * h + e;
+    const int key = kv ? 32 * kt + 16 * s + 8 * (e >> 2) + 4 * h + (e & 3) : 32 * kt + lc;
+    const float v = key < NK ? src[(long)dim * NK + key] : 0.f;
+    bad |= fabsf(v) >= 65504.f;
+    SPLIT_S(v, hi[e], lo[e]);
+  }
+  if (bad) atomicOr(range, 1);
+  _Float16* d = kvp + ((((((long)b * heads + hd) * nkt + kt) * 2 + kv) * 2 + s) * 2) * 512 + lane * 8;
+  *reinterpret_cast<h8*>(d) = hi;
+  *reinterpret_cast<h8*>(d + 512) = lo;
+}
+
+// The same attention with the fragments read straight from kvp (L2-resident: 28 query
+// blocks share a (b, head) slice): no LDS staging, no splits of K / V, no barriers.
+// Per 32-key tile the arithmetic is the staged kernel's, operation for operation.
+__global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __restrict__ Q,
+                                                             const _Float16* __restrict__ kvp, float* __restrict__ O,
+                                                             int C, int heads, int NQ, int NK, int nkt,
+                                                             int* __restrict__ range) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lc = lane & 31, h = lane >> 5;
+  const int nqb = (NQ + 127) / 128;
+  const int qb = blockIdx.x % nqb;
+  const int hd = (blockIdx.x / nqb) % heads;
+  const int b = blockIdx.x / (nqb * heads);
+  const int qi = qb * 128 + wave * 32 + lc;
+  const bool qvalid = qi < NQ;
+  const float* qp = Q + ((long)b * C + hd * 32) * NQ;
+  int bad = 0;
+  h8 qh[2], ql[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = qvalid ? qp[(long)(16 * s + 8 * h + e) * NQ + qi] * 0.17677669529663687f : 0.f;
+      bad |= fabsf(v) >= 65504.f;
+      SPLIT_S(v, qh[s][e], ql[s][e]);
+    }
+  const _Float16* base = kvp + ((long)b * heads + hd) * nkt * 8 * 512 + lane * 8;
+  // fragments of a tile: [k | v][s][hl], 1 KiB apart
+  h8 f[8], fn[8];
+  auto load = [&](int kt, h8* dst) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dst[i] = *reinterpret_cast<const h8*>(base + ((long)kt * 8 + i) * 512);
+  };
+  f32x16 oh, ox;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { oh[r] = 0.f; ox[r] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+  load(0, f);
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) load(kt + 1, fn);
+    const int j0 = 32 * kt;
+    f32x16 sh, sx, sxx;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { sh[r] = 0.f; sx[r] = 0.f; sxx[r] = 0.f; }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const h8 ah = f[2 * s], al = f[2 * s + 1];
+      sh = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[s], sh, 0, 0, 0);
+      sx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh[s], sx, 0, 0, 0);
+      sx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql[s], sx, 0, 0, 0);
+      sxx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ql[s], sxx, 0, 0, 0);
+    }
+    float cm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = j0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float sv = j < NK ? sh[r] + (sx[r] + sxx[r] * LO_DN) * LO_DN : -INFINITY;
+      sh[r] = sv;
+      cm = fmaxf(cm, sv);
+    }
+    cm = fmaxf(cm, __shfl_xor(cm, 32));
+    const float mn = fmaxf(m, cm);
+    if (mn != -INFINITY) {  // a fully padded tail tile (never the first) adds nothing
+      const float mnl = mn * 1.44269504088896341f;
+      const float alpha = __builtin_amdgcn_exp2f(fmaf(m, 1.44269504088896341f, -mnl));
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sh[r] = __builtin_amdgcn_exp2f(fmaf(sh[r], 1.44269504088896341f, -mnl));
+        ps += sh[r];
+      }
+      ps += __shfl_xor(ps, 32);
+      l = l * alpha + ps;
+      m = mn;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { oh[r] *= alpha; ox[r] *= alpha; }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        h8 ph, pl;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) SPLIT_S(sh[8 * s2 + e], ph[e], pl[e]);
+        const h8 vh = f[4 + 2 * s2], vl = f[5 + 2 * s2];
+        oh = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, oh, 0, 0, 0);
+        ox = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, ox, 0, 0, 0);
+        ox = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, ox, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = fn[i];
+  }
+  if (bad) atomicOr(range, 1);
+  if (qvalid) {
+    float* ob = O + ((long)b * C + hd * 32) * NQ + qi;
+    const float il = 1.f / l;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int dd = (r & 3) + 8 * (r >> 2) + 4 * h;
+      ob[(long)dd * NQ] = (oh[r] + ox[r] * LO_DN) * il;
+    }
+  }
+}
+
 }  // namespace
+
+size_t cross_kv_halves(int B, int C, int heads, int NK) {
+  return (size_t)B * heads * ((NK + 31) / 32) * 8 * 512;
+}
+
+bool cross_kv_split(hipStream_t s, const float* k, const float* v, _Float16* kvp, int B, int C, int heads, int NK) {
+  if (C != 32 * heads || NK < 1) return false;
+  const int nkt = (NK + 31) / 32;
+  const long total = (long)B * heads * nkt * 2 * 2 * 64;
+  hipLaunchKernelGGL(cross_kv_split_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, k, v, kvp, C, heads,
+                     NK, nkt, total, x3_range_ptr());
+  return true;
+}
+
+bool cross_attention_x3p(hipStream_t s, const float* q, const _Float16* kvp, float* o, int B, int C, int heads, int NQ,
+                         int NK) {
+  if (C != 32 * heads || NK < 1 || NQ < 1) return false;
+  const unsigned nblocks = (unsigned)(B * heads * ((NQ + 127) / 128));
+  hipLaunchKernelGGL(cross_attn_x3p_kernel, dim3(nblocks), dim3(256), 0, s, q, kvp, o, C, heads, NQ, NK,
+                     (NK + 31) / 32, x3_range_ptr());
+  return true;
+}
 
 bool cross_attention_x3(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,
                         int heads, int NQ, int NK) {

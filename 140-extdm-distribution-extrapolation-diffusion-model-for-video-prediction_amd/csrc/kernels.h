@@ -273,6 +273,12 @@ void cross_attention(hipStream_t s, const float* q, const float* k, const float*
 // f16x3 variant (cross_x3.hip); false if the shape is not covered (dim_head != 32)
 bool cross_attention_x3(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,
                         int heads, int NQ, int NK);
+// The same with K / V pre-split once (cross_kv_split, per sampling call) into MFMA fragments
+// kvp (cross_kv_halves halves): no staging in the per-step kernel.
+size_t cross_kv_halves(int B, int C, int heads, int NK);
+bool cross_kv_split(hipStream_t s, const float* k, const float* v, _Float16* kvp, int B, int C, int heads, int NK);
+bool cross_attention_x3p(hipStream_t s, const float* q, const _Float16* kvp, float* o, int B, int C, int heads, int NQ,
+                         int NK);
 
 void copy_view(hipStream_t s, const View& dst, const View& src);
 void maxpool_hw2(hipStream_t s, const View& dst, const View& src);

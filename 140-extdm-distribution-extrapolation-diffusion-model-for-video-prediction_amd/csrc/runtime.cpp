@@ -901,6 +901,16 @@ struct ExtdmHandle {
          ACT_RELU);
     conv(with_batch(kv_v, fea.B), fm, nullptr, P(c + ".linear_v.weight"), 1, 0, D(c + ".linear_v.bias"), nullptr,
          ACT_RELU);
+    // and split once into the cross kernel's MFMA fragments
+    if (!plan && kv_split_ok())
+      REQUIRE(cross_kv_split(s, kv_k.p, kv_v.p, kvp, fea.B, fea.C, cfg.heads, cfg.tc * cfg.fea_size * cfg.fea_size),
+              "TrajWarp: k / v split not covered");
+  }
+  // EXTDM_CROSS_STAGED=1: the per-step kernel stages and splits K / V itself (A/B)
+  bool kv_split_ok() const {
+    static const bool staged = [] { const char* v = getenv("EXTDM_CROSS_STAGED"); return v && v[0] && v[0] != '0'; }();
+    static const bool off = [] { const char* v = getenv("EXTDM_NO_X3_CROSS"); return v && v[0] && v[0] != '0'; }();
+    return kvp != nullptr && !staged && !off && x3_convs() && cfg.fea_ch == 32 * cfg.heads;
   }
   // xq = maxpool(1,2,2) of the tp frames' init_noise_conv output (u12:811)
   void trajwarp_q(const View& xq, const View& fea, const View& fp_out) {
@@ -914,7 +924,9 @@ struct ExtdmHandle {
     if (!plan) {
       static const bool off = [] { const char* v = getenv("EXTDM_NO_X3_CROSS"); return v && v[0] && v[0] != '0'; }();
       const bool x3 = !off && x3_convs() &&
-                      cross_attention_x3(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
+                      (kv_split_ok() ? cross_attention_x3p(s, q.p, kvp, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs)
+                                     : cross_attention_x3(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs,
+                                                          tc * fs * fs));
       if (!x3) cross_attention(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
     }
     View fm2p = alloc_cf(B, C, tp, fs, fs);
@@ -929,12 +941,16 @@ struct ExtdmHandle {
   // k / v of fm, and for ada / ada_u22 the resized cond_adaptor + cond_temporal_attn
   // features (ada.py:1035-1036), which depend on cond_fea only.
   View r_all, kv_k, kv_v, fup_all;
+  _Float16* kvp = nullptr;  // k / v as pre-split MFMA fragments (cross_kv_split)
   void alloc_cond_cache() {
     const int Bm = cfg.max_batch, T = frames(), L = cfg.latent, fs = cfg.fea_size;
     r_all = cf_view(dmalloc((size_t)Bm * cfg.dim * T * L * L * 4), Bm, cfg.dim, T, L, L);
     if (cfg.arch == EXTDM_ARCH_U12) {
       kv_k = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * cfg.tc * fs * fs * 4), Bm, cfg.fea_ch, cfg.tc, fs, fs);
       kv_v = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * cfg.tc * fs * fs * 4), Bm, cfg.fea_ch, cfg.tc, fs, fs);
+      if (cfg.fea_ch == 32 * cfg.heads)
+        kvp = reinterpret_cast<_Float16*>(
+            dmalloc(cross_kv_halves(Bm, cfg.fea_ch, cfg.heads, cfg.tc * fs * fs) * sizeof(_Float16)));
     }
     if (cfg.arch == EXTDM_ARCH_ADA || cfg.arch == EXTDM_ARCH_ADA_U22)
       fup_all = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * T * L * L * 4), Bm, cfg.fea_ch, T, L, L);
