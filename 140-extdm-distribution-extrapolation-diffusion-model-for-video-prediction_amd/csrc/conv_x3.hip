@@ -646,15 +646,25 @@ void launch_ns(hipStream_t s, const X3Args& a, unsigned ntiles) {
 // (84 KB of LDS), so it splits only below 128 workgroups and up to 256 in total (a second
 // round of workgroups cost more than the shorter K loops saved: 70 -> 80 us at 256 x 2);
 // the 1x1 128-row tile (several workgroups per CU) splits below 384, up to 512. Slices keep
-// >= 2 channel blocks, and the partials (S x workgroups x tile floats) must fit the
-// workspace. EXTDM_NO_SPLITK=1 turns it off (A/B).
-bool split_k(X3Args& a, unsigned ntiles, int tile_elems, const ConvEpi& e, long max_wg, long max_total) {
+// >= 2 channel blocks. The slice count is a function of the per-sample geometry only (the
+// workgroup count at the reference batch 64), never of the batch: a clip's result must
+// not depend on the shard it lands in (tiles never straddle samples here, T % NP == 0).
+// EXTDM_NO_SPLITK=1 turns it off (A/B).
+int split_slices(const X3Args& a, unsigned ntiles, long max_wg, long max_total) {
   static const bool off = [] { const char* v = getenv("EXTDM_NO_SPLITK"); return v && v[0] && v[0] != '0'; }();
-  const long nwg = (long)ntiles * ((a.Cout + 127) / 128);
-  if (off || !e.split_ws || nwg >= max_wg || a.ncgb < 4) return false;
-  int S = (int)std::min<long>(a.ncgb / 2, max_total / nwg);
-  while (S >= 2 && (size_t)S * nwg * tile_elems * sizeof(float) > e.split_ws_bytes) --S;
-  if (S < 2) return false;
+  const int B = a.P / a.T;
+  if (off || a.ncgb < 4 || a.T % a.NP != 0 || B < 1 || (long)ntiles % B != 0) return 0;
+  const long nwg64 = (long)ntiles / B * ((a.Cout + 127) / 128) * 64;
+  if (nwg64 >= max_wg) return 0;
+  const int S = (int)std::min<long>(a.ncgb / 2, max_total / nwg64);
+  return S >= 2 ? S : 0;
+}
+size_t split_bytes(const X3Args& a, unsigned ntiles, int S) {
+  return S ? (size_t)S * ntiles * ((a.Cout + 127) / 128) * 128 * 128 * sizeof(float) : 0;
+}
+bool split_k(X3Args& a, unsigned ntiles, const ConvEpi& e, long max_wg, long max_total) {
+  const int S = split_slices(a, ntiles, max_wg, max_total);
+  if (!S || !e.split_ws || split_bytes(a, ntiles, S) > e.split_ws_bytes) return false;
   a.part = e.split_ws;
   a.nsplit = S;
   return true;
@@ -782,7 +792,7 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     else launch<3, 1, 64, 256, 1, 4, 4, 2>(s, a, ntiles);
   }
   else if (ks == 3 && tl.bm == 128) {
-    if (split_k(a, ntiles, 128 * 128, epi, 128, 256)) {
+    if (split_k(a, ntiles, epi, 128, 256)) {
       launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, false, false, 1>(s, a, ntiles);
       launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, false, false, 2>(s, a, ntiles);
     } else {
@@ -791,7 +801,7 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   }
   else if (ks == 1 && tl.bm == 64) launch<1, 1, 64, 128, 2, 4, 4, 2>(s, a, ntiles);
   else if (ks == 1 && tl.bm == 128) {
-    if (split_k(a, ntiles, 128 * 128, epi, 384, 512)) {
+    if (split_k(a, ntiles, epi, 384, 512)) {
       launch_sp<1, 1, 128, 128, 2, 2, 4, 2, true, 1, false, false, 1>(s, a, ntiles);
       launch_sp<1, 1, 128, 128, 2, 2, 4, 2, true, 1, false, false, 2>(s, a, ntiles);
     } else {
@@ -811,6 +821,25 @@ bool conv_x3_covers(const View& out, const View& in0, const View* in1, const Pac
                        (w.xbn != 512 && ((ks == 7 && w.xbm == 64) || (ks == 3 && (w.xbm == 64 || w.xbm == 128)) ||
                                          (ks == 1 && (w.xbm == 64 || w.xbm == 128))));
   return tile_ok && x3_setup(out, in0, in1, w, ConvEpi{}, a, ntiles, nullptr);
+}
+
+size_t conv_x3_split_bytes(const View& out, const View& in0, const View* in1, const PackedW& w) {
+  X3Args a;
+  unsigned ntiles = 0;
+  if (w.mode != MODE_CONV || w.KH != w.KW || !x3_setup(out, in0, in1, w, ConvEpi{}, a, ntiles, nullptr)) return 0;
+  if (w.xbn == 512 || w.xbm != 128) return 0;
+  if (w.KH == 3) return split_bytes(a, ntiles, split_slices(a, ntiles, 128, 256));
+  if (w.KH == 1) return split_bytes(a, ntiles, split_slices(a, ntiles, 384, 512));
+  return 0;
+}
+
+size_t conv_x3_op_split_bytes(const View& out, const PackedW& w, int C) {
+  if (!conv_x3_op_supported(out, w, C, 1) || w.xbm != 128) return 0;
+  X3Args a;
+  unsigned ntiles = 0;
+  const View g = cf_view(nullptr, out.B, C, out.T, out.H, out.W);
+  if (!x3_setup(out, g, nullptr, w, ConvEpi{}, a, ntiles, nullptr)) return 0;
+  return split_bytes(a, ntiles, split_slices(a, ntiles, 128, 256));
 }
 
 size_t x3op_halves(int B, int C, int T, int H, int W, int pad) {
@@ -854,7 +883,7 @@ bool conv_x3_forward_op(hipStream_t s, const View& out, const X3Op& in, const Pa
   if (w.xbm == 64) {
     if (x3_v3() == 1) launch_sp<3, 3, 64, 256, 1, 4, 8, 2, true, 1, true>(s, a, ntiles);
     else launch_sp<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true>(s, a, ntiles);
-  } else if (split_k(a, ntiles, 128 * 128, epi, 128, 256)) {
+  } else if (split_k(a, ntiles, epi, 128, 256)) {
     launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true, false, 1>(s, a, ntiles);
     launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true, false, 2>(s, a, ntiles);
   } else {

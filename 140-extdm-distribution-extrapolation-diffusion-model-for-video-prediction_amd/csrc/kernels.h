@@ -145,6 +145,9 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
                      const ConvEpi& epi, int* stats_slots = nullptr);
 // Whether conv_x3_forward covers this stride-1 'same' conv (no launch).
 bool conv_x3_covers(const View& out, const View& in0, const View* in1, const PackedW& w);
+// Split-K partial bytes the conv will use (0: no split) -- ConvEpi::split_ws must hold them.
+size_t conv_x3_split_bytes(const View& out, const View& in0, const View* in1, const PackedW& w);
+size_t conv_x3_op_split_bytes(const View& out, const PackedW& w, int C);
 // Pre-split f16x3 conv input ("operand") of an activation [B][C][T][H][W]: hi / lo fp16
 // halves as [hl][c8][C/16][B*T][H+2*pad][W+2*pad][8] with a zero ring of width pad:
 // channel 16*cg + 8*c8 + e of a padded position is element e of its 16-B record in

@@ -101,9 +101,6 @@ struct ExtdmHandle {
   // workspace
   Arena arena;
   double* partials = nullptr;
-  // split-K partials of the direct convs (ConvEpi::split_ws): 512 workgroups x 128 x 128 fp32
-  float* split_ws = nullptr;
-  static constexpr size_t kSplitWsBytes = (size_t)512 * 128 * 128 * sizeof(float);
   // EXTDM_NO_GN_FUSE=1: separate GroupNorm statistics pass after every ResnetBlock conv
   const bool fuse_gn_stats = [] { const char* v = getenv("EXTDM_NO_GN_FUSE"); return !(v && v[0] && v[0] != '0'); }();
   // EXTDM_NO_RES_GN=1: block2's GroupNorm applied in place before res_conv (A/B)
@@ -500,6 +497,14 @@ struct ExtdmHandle {
             "conv: batch of an operand does not match the output");
     REQUIRE(w.mode != MODE_CONV || stride != 1 || (in0.T == out.T && (!in1 || in1->T == out.T)),
             "conv: frame count of an operand does not match the output");
+    // split-K partials (conv_x3, launches that leave CUs idle) from the arena, for this conv
+    Scope sc(arena);
+    float* split_ws = nullptr;
+    size_t split_bytes = 0;
+    if (x3_convs() && stride == 1 && pad == w.KH / 2) {
+      split_bytes = conv_x3_split_bytes(out, in0, in1, w);
+      if (split_bytes) split_ws = arena.alloc(split_bytes / sizeof(float));
+    }
     if (plan) return 0;
     ConvEpi e;
     e.bias = bias;
@@ -511,7 +516,7 @@ struct ExtdmHandle {
     e.post_shift = psh;
     e.post_per_channel = per_channel;
     e.split_ws = split_ws;
-    e.split_ws_bytes = split_ws ? kSplitWsBytes : 0;
+    e.split_ws_bytes = split_bytes;
     return conv_forward(s, out, in0, in1, w, stride, pad, e);
   }
 
@@ -539,13 +544,15 @@ struct ExtdmHandle {
         groupnorm_silu_x3op(s, h1, op, 8, D(p + ".block1.norm.weight"), D(p + ".block1.norm.bias"),
                             has_mlp ? film : nullptr, has_mlp ? film_row[p] : 0, film_nt, t_batch, partials, sp1);
       h2 = alloc_cf(B, C, T, Hh, Ww);
+      const size_t sb2 = conv_x3_op_split_bytes(h2, w2, C);
+      float* sw2 = sb2 ? arena.alloc(sb2 / sizeof(float)) : nullptr;
       if (!plan) {
         ConvEpi e;
         e.bias = D(p + ".block2.proj.bias");
         e.stats = st;
         e.stats_groups = 8;
-        e.split_ws = split_ws;
-        e.split_ws_bytes = split_ws ? kSplitWsBytes : 0;
+        e.split_ws = sw2;
+        e.split_ws_bytes = sb2;
         REQUIRE(conv_x3_forward_op(s, h2, op, w2, e, &sp2), "block2 conv: operand input not covered");
       }
     } else {
@@ -562,8 +569,6 @@ struct ExtdmHandle {
       ConvEpi e;
       e.bias = D(p + ".res_conv.bias");
       e.res = h2.p; e.res_sb = h2.sb; e.res_sc = h2.sc; e.res_st = h2.st;
-      e.split_ws = split_ws;
-      e.split_ws_bytes = split_ws ? kSplitWsBytes : 0;
       e.res_aff = groupnorm_affine(s, h2, 8, D(p + ".block2.norm.weight"), D(p + ".block2.norm.bias"), partials, sp2);
       REQUIRE(conv_x3_forward(s, out, in0, in1, *wr, e), "res_conv: f16x3 direct conv not covered");
     } else if (wr) {
@@ -1636,7 +1641,6 @@ struct ExtdmHandle {
     eps_buf = dmalloc((size_t)B * n * sizeof(float));
     // GroupNorm: [B][8 groups][64 slots][sum, sumsq], then (mean, rstd) per (b, group),
     // then the [B][C <= 512] (scale, shift) table of groupnorm_affine
-    split_ws = reinterpret_cast<float*>(dmalloc(kSplitWsBytes));
     partials = reinterpret_cast<double*>(dmalloc(((size_t)B * 8 * 64 * 2 + (size_t)B * 8 + (size_t)B * 512) * sizeof(double)));
     t_batch = reinterpret_cast<int*>(dmalloc((size_t)std::max(B, 1) * sizeof(int)));
     step_ctr = reinterpret_cast<int*>(dmalloc(sizeof(int) * 4));
