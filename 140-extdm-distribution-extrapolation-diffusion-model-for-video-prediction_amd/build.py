@@ -23,7 +23,13 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=o
 # work between MFMAs) must not be SLP-vectorised: at -O3 the SLP pass turns their
 # scalar fp32 arithmetic into v_pk_mul_f32 / v_pk_add_f32 pairs (DESIGN.md §4.0 build
 # note), which also pushes the 8-wave C = 64 kernels past 256 VGPRs into scratch.
-PER_FILE = {'stw_x3.hip': ['-fno-slp-vectorize'], 'cross_x3.hip': ['-fno-slp-vectorize']}
+# The attention kernels run softmax / splits on MFMA accumulators: with hipcc's default
+# AGPR accumulators every such value is copied out (v_accvgpr_read) and back (the cross
+# kernel's key-tile loop: 112 copies in 441 instructions); the VGPR form of the MFMAs keeps
+# them in VGPRs (the convs' accumulators only meet VALU in the epilogue and keep AGPRs).
+VGPR_MFMA = ['-mllvm', '-amdgpu-mfma-vgpr-form=1']
+PER_FILE = {'stw_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA, 'cross_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA,
+            'attn_core.hip': VGPR_MFMA}
 OPT = {}
 
 

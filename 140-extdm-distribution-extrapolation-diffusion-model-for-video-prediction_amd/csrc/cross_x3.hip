@@ -231,6 +231,20 @@ __global__ __launch_bounds__(256) void cross_kv_split_kernel(const float* __rest
 // The same attention with the fragments read straight from kvp (L2-resident: 28 query
 // blocks share a (b, head) slice): no LDS staging, no splits of K / V, no barriers.
 // Per 32-key tile the arithmetic is the staged kernel's, operation for operation.
+// scaled-lo split of a pair into elements e, e + 1 (compiler-visible: the values come
+// from and go to MFMAs): hi = fp16 pair, lo = fp16((v - hi) * 2^11) via v_fma_mix_f32
+__device__ __forceinline__ void split2s(float a, float b, h8& hi, h8& lo, int e) {
+  f16x2_t ph, pl;
+  const float a_ = split_src(a), b_ = split_src(b);
+  ph = __builtin_convertvector((f32x2_t){a_, b_}, f16x2_t);
+  const float one = split_src(1.0f);
+  const float la = __builtin_fmaf(-(float)ph.x, one, a_) * LO_UP;
+  const float lb = __builtin_fmaf(-(float)ph.y, one, b_) * LO_UP;
+  pl = __builtin_convertvector((f32x2_t){la, lb}, f16x2_t);
+  hi[e] = ph.x; hi[e + 1] = ph.y;
+  lo[e] = pl.x; lo[e + 1] = pl.y;
+}
+
 __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __restrict__ Q,
                                                              const _Float16* __restrict__ kvp, float* __restrict__ O,
                                                              int C, int heads, int NQ, int NK, int nkt,
@@ -281,10 +295,12 @@ __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __rest
       sxx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ql[s], sxx, 0, 0, 0);
     }
     float cm = -INFINITY;
+    const bool full = j0 + 32 <= NK;  // wave-uniform: no key mask in a full tile
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int j = j0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float sv = j < NK ? sh[r] + (sx[r] + sxx[r] * LO_DN) * LO_DN : -INFINITY;
+      const float sc = fmaf(fmaf(sxx[r], LO_DN, sx[r]), LO_DN, sh[r]);
+      const float sv = (full || j < NK) ? sc : -INFINITY;
       sh[r] = sv;
       cm = fmaxf(cm, sv);
     }
@@ -308,7 +324,7 @@ __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __rest
       for (int s2 = 0; s2 < 2; ++s2) {
         h8 ph, pl;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) SPLIT_S(sh[8 * s2 + e], ph[e], pl[e]);
+        for (int e = 0; e < 8; e += 2) split2s(sh[8 * s2 + e], sh[8 * s2 + e + 1], ph, pl, e);
         const h8 vh = f[4 + 2 * s2], vl = f[5 + 2 * s2];
         oh = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, oh, 0, 0, 0);
         ox = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, ox, 0, 0, 0);
