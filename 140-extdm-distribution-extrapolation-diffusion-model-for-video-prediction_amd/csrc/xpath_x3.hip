@@ -156,13 +156,16 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
 // and 4 m32 tiles (128 output channels); K = 3 ch x 4 row pairs x 8 columns (7 used):
 // lane half h takes row 2*dyp + h of the pair. Pool: rows within the lane (nt), columns
 // with the partner lane (lane ^ 1, same rows of the accumulator).
+constexpr int NP_MW = 2;
 __global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
-  constexpr int MW = 4;  // m32 tiles per wave
+  // m32 tiles per wave: 2 (64 rows), so accumulators + operands fit two waves per SIMD
+  // (MW = 4 took 158 VGPRs + 128 AGPRs: one wave per SIMD, every k-step's L2 loads exposed)
+  constexpr int MW = NP_MW;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lc = lane & 31, h = lane >> 5;
   const int L = a.L, Lh = L / 2;
   const int nrp = a.F * Lh;
   const int unit = blockIdx.x * 4 + wave;  // (row pair, m-quarter)
-  const int nmq = (a.Cout + 127) / 128;
+  const int nmq = (a.Cout + 32 * MW - 1) / (32 * MW);
   if (unit >= nrp * nmq) return;
   const int rp = unit / nmq, mq = unit - rp * nmq;
   const int f = rp / Lh, yp = rp - f * Lh;
@@ -180,7 +183,7 @@ __global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
   const _Float16* wq = a.w + (long)mq * MW * 1024 + lane * 8;
   const int M32 = (a.Cout + 31) / 32;
   int bad = 0;
-#pragma unroll 1
+#pragma unroll 2
   for (int ks = 0; ks < 12; ++ks) {
     const int ci = ks / 4, dy = 2 * (ks % 4) + h;
     h8 ah[MW], al[MW];
@@ -225,7 +228,7 @@ bool noise_pool_x3_forward(hipStream_t s, const View& out, const View& x, const 
   a.T = x.T; a.L = L; a.F = x.B * x.T;
   a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
   a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.bias = bias; a.range = x3_range_ptr();
-  const long units = (long)a.F * (L / 2) * ((out.C + 127) / 128);
+  const long units = (long)a.F * (L / 2) * ((out.C + 32 * NP_MW - 1) / (32 * NP_MW));
   hipLaunchKernelGGL(noise_pool_x3_kernel, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, s, a);
   return true;
 }
