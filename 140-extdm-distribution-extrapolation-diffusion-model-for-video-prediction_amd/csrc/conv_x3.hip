@@ -700,7 +700,13 @@ X3Tile x3_tile(int ks, int cout) {
     if (cout <= 64) { t.bm = 64; t.bn = bn3 == 512 ? 512 : 256; } else { t.bm = 128; t.bn = 128; }
     t.ng = 1;
   }
-  else if (ks == 1) { t.bm = cout <= 64 ? 64 : 128; t.bn = 128; t.ng = 2; }
+  else if (ks == 1) {
+    // Cout a multiple of 256: one 256-row m-tile (8 waves), so each pixel tile's input is
+    // staged once instead of once per 128 rows. EXTDM_X3_BM1=128 restores 128-row tiles.
+    static const int bm1 = [] { const char* v = getenv("EXTDM_X3_BM1"); return v ? atoi(v) : 256; }();
+    t.bm = cout <= 64 ? 64 : ((bm1 == 256 && cout % 256 == 0) ? 256 : 128);
+    t.bn = 128; t.ng = 2;
+  }
   return t;
 }
 
@@ -773,6 +779,7 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     if (ks != 1 || !epi.res || tl.bn != 128) return false;
     if (tl.bm == 64) launch_sp<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, true>(s, a, ntiles);
     else if (tl.bm == 128) launch_sp<1, 1, 128, 128, 2, 2, 4, 2, true, 1, false, true>(s, a, ntiles);
+    else if (tl.bm == 256) launch_sp<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, true>(s, a, ntiles);
     else return false;
     return true;
   }
@@ -800,6 +807,7 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     }
   }
   else if (ks == 1 && tl.bm == 64) launch<1, 1, 64, 128, 2, 4, 4, 2>(s, a, ntiles);
+  else if (ks == 1 && tl.bm == 256) launch<1, 1, 256, 128, 2, 2, 8, 2>(s, a, ntiles);
   else if (ks == 1 && tl.bm == 128) {
     if (split_k(a, ntiles, epi, 384, 512)) {
       launch_sp<1, 1, 128, 128, 2, 2, 4, 2, true, 1, false, false, 1>(s, a, ntiles);
@@ -819,7 +827,7 @@ bool conv_x3_covers(const View& out, const View& in0, const View* in1, const Pac
   const int ks = w.KH;
   const bool tile_ok = (w.xbn == 512 && w.xbm == 64 && (ks == 7 || ks == 3)) ||
                        (w.xbn != 512 && ((ks == 7 && w.xbm == 64) || (ks == 3 && (w.xbm == 64 || w.xbm == 128)) ||
-                                         (ks == 1 && (w.xbm == 64 || w.xbm == 128))));
+                                         (ks == 1 && (w.xbm == 64 || w.xbm == 128 || w.xbm == 256))));
   return tile_ok && x3_setup(out, in0, in1, w, ConvEpi{}, a, ntiles, nullptr);
 }
 
