@@ -199,7 +199,10 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
         kf[t][s].set(kv + 8 * s, bad);
       }
     }
-    __syncthreads();  // Vs of this head visible to the wave's V^T reads (and to nobody else)
+    // Vs[wave] is private to the wave: a wave-level fence + barrier orders its writes before
+    // the V^T reads (a block barrier here would diverge when heads % 4 != 0)
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int qt = 0; qt < NT; ++qt) {
       // ---- scores S^T[kt] of query tile qt, softmax over the keys of each query ----
@@ -265,7 +268,8 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
         for (int r = 0; r < 16; ++r) ob[(long)(hd * 32 + dof(r, h)) * osc] = out[r];
       }
     }
-    __syncthreads();  // Vs reuse by the next head
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // Vs reuse by the wave's next head
+    __builtin_amdgcn_wave_barrier();
   }
   if (X3 && bad) atomicOr(range_flag, 2);
 }

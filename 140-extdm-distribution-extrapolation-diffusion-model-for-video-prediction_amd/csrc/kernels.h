@@ -52,6 +52,16 @@ __device__ __forceinline__ void split2c(float a, float b, f16x2_t& hi, f16x2_t& 
   const float lb = __builtin_fmaf(-(float)hi.y, one, b);
   lo = __builtin_convertvector((f32x2_t){la, lb}, f16x2_t);
 }
+// The same split with lo produced in fp16 directly: each remainder as (fp16)fma(-hi, 1, v)
+// is one v_fma_mixlo_f16 / v_fma_mixhi_f16 (3 VALU per pair). v - hi is exact in fp32, so
+// the single rounding to fp16 gives the bits split2c gives. Needs -fno-slp-vectorize (the
+// SLP pass otherwise packs the two fmas into a v_pk_fma_f32 and converts afterwards).
+__device__ __forceinline__ void split2m(float a, float b, f16x2_t& hi, f16x2_t& lo) {
+  hi = __builtin_convertvector((f32x2_t){a, b}, f16x2_t);
+  const float one = split_src(1.0f);
+  lo.x = (_Float16)__builtin_fmaf(-(float)hi.x, one, a);
+  lo.y = (_Float16)__builtin_fmaf(-(float)hi.y, one, b);
+}
 // m = max(m, |a|, |b|) in one v_max3_f32 (the fp16-range check of the split values;
 // the same hazard rule as split2)
 __device__ __forceinline__ void amax2(float& m, float a, float b) {
@@ -238,12 +248,13 @@ bool temporal_fused(hipStream_t s, const View& x, const View& out, const AttnGeo
 // kernel header); wsc = {2^-sq, 2^-sk, 2^-sv, 2^-sproj} undoes the power-of-two pre-scaling.
 bool attn_x3_supported(int C, int ntok, int dim_head, int heads);
 int attn_x3_unit_halves(int C);
+// mbias: [npat][8][32][32] bias + masks per window class (stw_x3.hip kernel header).
 bool stw_x3(hipStream_t s, const View& x, const AttnGeom& g, int heads, int dim_head, const float* gamma,
-            const void* wpk, const float* wsc, const float* bp, const float* bias_dense, int bstride,
+            const void* wpk, const float* wsc, const float* bp, const float* mbias, int npat,
             const float* rcos, const float* rsin, float q_scale);
 bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, int dim_head,
                  const float* gamma, const float* ln_w, const float* ln_b, const void* wpk, const float* wsc,
-                 const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale);
+                 const float* mbias, const float* rcos, const float* rsin, float q_scale);
 // TrajWarp cross-attention (u12:719-773): q [B][256][NQ], k,v [B][256][NK].
 // f16x3 implicit-GEMM conv (conv_gemm_x3.hip): every mode / kernel size of conv_forward's
 // fp32 GEMM; false if the weight has no f16x3 GEMM packing

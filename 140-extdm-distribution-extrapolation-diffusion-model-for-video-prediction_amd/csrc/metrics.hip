@@ -10,6 +10,10 @@
 #include <cmath>
 #include <stdexcept>
 
+#include <mutex>
+#include <stdexcept>
+#include <string>
+
 #include "kernels.h"
 
 namespace extdm {
@@ -142,20 +146,29 @@ void frame_metrics(hipStream_t s, const float* a, const float* b, int N, int T, 
   if (N < 1 || T < 1 || (C != 1 && C != 3))
     throw std::invalid_argument("frame_metrics: frames must have 1 or 3 channels (calculate_ssim.py:33-41)");
   if (H <= 2 * SSIM_R || W <= 2 * SSIM_R) throw std::invalid_argument("frame_metrics: frames smaller than 11x11");
-  if ((size_t)(STRIP + 2 * SSIM_R) * W * 2 * sizeof(float) > 150 * 1024)
-    throw std::invalid_argument("frame_metrics: rows wider than the LDS strip (W > 1920)");
   const int nf = N * T;
-  hipLaunchKernelGGL(psnr_kernel, dim3(nf), dim3(256), 0, s, a, b, T, C, H, W, sN, sT, sC, psnr);
   const int nstrip = (H - 2 * SSIM_R + STRIP - 1) / STRIP;
   const size_t lds = (size_t)(STRIP + 2 * SSIM_R) * W * 2 * sizeof(float);
-  // dynamic LDS up to 150 KiB (the kernel's static __shared__ takes the rest of 160)
-  static bool attr = false;
-  if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&ssim_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            150 * 1024) != hipSuccess)
-      throw std::runtime_error("frame_metrics: cannot raise the SSIM kernel's LDS limit");
-    attr = true;
-  }
+  // the device's per-workgroup LDS less the kernel's static __shared__, read once per device
+  // (160 KiB on gfx950: dynamic strips up to ~150 KiB, rows up to ~1900 px)
+  struct Dev { std::once_flag once; size_t max_dyn = 0; hipError_t err = hipSuccess; };
+  static Dev devs[64];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  Dev& dv = devs[dev & 63];
+  std::call_once(dv.once, [&] {
+    int smem = 0;
+    hipFuncAttributes fa{};
+    (void)hipDeviceGetAttribute(&smem, hipDeviceAttributeMaxSharedMemoryPerBlock, dev);
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&ssim_kernel));
+    dv.max_dyn = smem > (int)fa.sharedSizeBytes ? (size_t)smem - fa.sharedSizeBytes : 0;
+    dv.err = hipFuncSetAttribute(reinterpret_cast<const void*>(&ssim_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)dv.max_dyn);
+  });
+  if (dv.err != hipSuccess) throw std::runtime_error("frame_metrics: cannot raise the SSIM kernel's LDS limit");
+  if (lds > dv.max_dyn)
+    throw std::invalid_argument("frame_metrics: rows wider than the device's LDS strip (W = " + std::to_string(W) + ")");
+  hipLaunchKernelGGL(psnr_kernel, dim3(nf), dim3(256), 0, s, a, b, T, C, H, W, sN, sT, sC, psnr);
   hipLaunchKernelGGL(ssim_kernel, dim3(nf, C, nstrip), dim3(256), lds, s, a, b, T, C, H, W, sN, sT, sC, nstrip, work);
   const double npix = (double)(H - 2 * SSIM_R) * (W - 2 * SSIM_R);
   hipLaunchKernelGGL(ssim_finalize_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, work, nf, C, nstrip, npix, ssim);

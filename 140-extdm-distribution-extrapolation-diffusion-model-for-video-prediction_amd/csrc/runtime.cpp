@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <cstring>
 #include <memory>
@@ -97,6 +98,10 @@ struct ExtdmHandle {
   float* rope_sin = nullptr;
   std::unordered_map<std::string, float*> bias_dense;  // STW layer prefix -> [heads][32][32]
   float* time_bias = nullptr;                            // [heads][32][32]
+  // host copies for the f16x3 kernels' bias + mask tables (stw_mask_bias)
+  std::unordered_map<std::string, std::pair<std::vector<float>, int>> bias_host;  // prefix -> (dense, stride)
+  std::vector<float> time_bias_host;
+  std::unordered_map<std::string, std::pair<float*, int>> mask_bias;  // prefix|geometry -> (table, npat)
 
   // workspace
   Arena arena;
@@ -602,6 +607,77 @@ struct ExtdmHandle {
     return g;
   }
 
+  // Bias + mask tables of the f16x3 fused attention kernels (stw_x3.hip):
+  // [npat][heads][32 queries][32 keys] = the dense relative-position bias (leading N x N
+  // block, u12:476) + -100 where a shifted window's region labels differ (compute_mask,
+  // u12:414-436, applied after the bias as attn + mask) and -inf for keys past the
+  // window's N tokens. A shifted layer's windows fall in 8 classes — bit d set for the
+  // last window along a shifted dim d, the only one whose tokens carry two labels — and
+  // each class has its own table; an unshifted layer has one.
+  static int region_label(int c, int P, int w, int s) { return s == 0 ? 2 : c >= P - s ? 2 : c >= P - w ? 1 : 0; }
+  const float* stw_mask_bias(const std::string& p, const AttnGeom& g, int& npat) {
+    const std::string key = p + "|" + std::to_string(g.ws0) + "," + std::to_string(g.ws1) + "," + std::to_string(g.ws2) +
+                            "|" + std::to_string(g.ss0) + "," + std::to_string(g.ss1) + "," + std::to_string(g.ss2) +
+                            "|" + std::to_string(g.Dp) + "," + std::to_string(g.Hp) + "," + std::to_string(g.Wp);
+    auto it = mask_bias.find(key);
+    if (it != mask_bias.end()) { npat = it->second.second; return it->second.first; }
+    const auto& bh = bias_host.at(p);
+    const int nh = cfg.heads, st = bh.second, N = g.ws0 * g.ws1 * g.ws2;
+    REQUIRE(N <= 32 && nh == 8, "bias + mask table: window of more than 32 tokens");
+    const bool shifted = (g.ss0 | g.ss1 | g.ss2) != 0;
+    npat = shifted ? 8 : 1;
+    const int ws[3] = {g.ws0, g.ws1, g.ws2}, ss[3] = {g.ss0, g.ss1, g.ss2}, P[3] = {g.Dp, g.Hp, g.Wp};
+    std::vector<float> t((size_t)npat * nh * 1024, 0.f);
+    for (int pat = 0; pat < npat; ++pat) {
+      int lab[32] = {0};
+      for (int tk = 0; tk < N; ++tk) {
+        const int tc[3] = {tk / (ws[1] * ws[2]), (tk / ws[2]) % ws[1], tk % ws[2]};
+        int l = 0;
+        for (int d = 0; d < 3; ++d) {
+          const int wi = ((pat >> d) & 1) ? P[d] / ws[d] - 1 : 0;
+          l = l * 3 + region_label(wi * ws[d] + tc[d], P[d], ws[d], ss[d]);
+        }
+        lab[tk] = l;
+      }
+      for (int hd = 0; hd < nh; ++hd)
+        for (int i = 0; i < 32; ++i)
+          for (int j = 0; j < 32; ++j) {
+            float v = 0.f;
+            if (j >= N) v = -INFINITY;
+            else if (i < N) {
+              v = bh.first[((size_t)hd * st + i) * st + j];
+              if (shifted && lab[i] != lab[j]) v += -100.f;
+            }
+            t[(((size_t)pat * nh + hd) * 32 + i) * 32 + j] = v;
+          }
+    }
+    float* d = dmalloc(t.size() * 4);
+    HIPCHK(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    mask_bias[key] = {d, npat};
+    return d;
+  }
+  // temporal attention (one table): T5 bias of (query frame, key frame), -inf for another
+  // pixel's frames and for key frames >= D (32-token groups of 32 / per pixels)
+  const float* temporal_mask_bias(const AttnGeom& g) {
+    const std::string key = "temporal|" + std::to_string(g.D);
+    auto it = mask_bias.find(key);
+    if (it != mask_bias.end()) return it->second.first;
+    const int nh = cfg.heads, per = g.D <= 16 ? 16 : 32;
+    REQUIRE(nh == 8 && g.D <= 32, "temporal bias + mask table: shape");
+    std::vector<float> t((size_t)nh * 1024, 0.f);
+    for (int hd = 0; hd < nh; ++hd)
+      for (int i = 0; i < 32; ++i)
+        for (int j = 0; j < 32; ++j) {
+          const int pi = i / per, ti = i % per, pj = j / per, tj = j % per;
+          t[((size_t)hd * 32 + i) * 32 + j] =
+              (pi != pj || tj >= g.D) ? -INFINITY : time_bias_host[(size_t)hd * 1024 + ti * 32 + tj];
+        }
+    float* d = dmalloc(t.size() * 4);
+    HIPCHK(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    mask_bias[key] = {d, 1};
+    return d;
+  }
+
   // Packed weights of the fused attention kernels (stw_fused.hip header): qkv rows
   // in 32-row units (one head of dim 32 / two heads of dim 16).
   float* packed_stw_qkv(const std::string& n) {
@@ -748,9 +824,11 @@ struct ExtdmHandle {
     if (fused_x3) {
       const std::string a = p + ".fn.fn.attn";
       const AttnX3W& w = packed_attn_x3(a + ".qkv.weight", a + ".proj.weight");
+      int npat = 1;
+      const float* mb = stw_mask_bias(p, g, npat);
       if (plan) return;
       REQUIRE(stw_x3(s, x, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), w.w, w.sc, D(a + ".proj.bias"),
-                     bias_dense.at(p), bstride, rope_cos, rope_sin, q_scale()),
+                     mb, npat, rope_cos, rope_sin, q_scale()),
               "f16x3 STW launch rejected");
       return;
     }
@@ -804,9 +882,10 @@ struct ExtdmHandle {
     }
     if (fused_x3) {
       const AttnX3W& w = packed_attn_x3(a + ".attn.to_qkv.weight", a + ".attn.to_out.weight");
+      const float* mb = temporal_mask_bias(g);
       if (plan) return;
       REQUIRE(temporal_x3(s, x, out, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), D(a + ".norm.weight"),
-                          D(a + ".norm.bias"), w.w, w.sc, time_bias, 32, rope_cos, rope_sin, q_scale()),
+                          D(a + ".norm.bias"), w.w, w.sc, mb, rope_cos, rope_sin, q_scale()),
               "f16x3 temporal attention launch rejected");
       return;
     }
@@ -1552,6 +1631,7 @@ struct ExtdmHandle {
       float* dd = dmalloc(d.size() * 4);
       HIPCHK(hipMemcpy(dd, d.data(), d.size() * 4, hipMemcpyHostToDevice));
       bias_dense[p] = dd;
+      bias_host[p] = {std::move(d), st};
     }
     // temporal T5 relative-position bias (RelativePositionBias, u12:42-79), max_distance 32
     {
@@ -1579,6 +1659,7 @@ struct ExtdmHandle {
         }
       time_bias = dmalloc(d.size() * 4);
       HIPCHK(hipMemcpy(time_bias, d.data(), d.size() * 4, hipMemcpyHostToDevice));
+      time_bias_host = std::move(d);
     }
     HIPCHK(hipDeviceSynchronize());
   }
@@ -1923,6 +2004,55 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     // layers 1-4: ResnetBlock convs (u12:165, 200) at levels 0-2 and a level-0 res_conv,
     // fp32 input staged by the conv; layer 5: the level-0 block2 conv as the forward issues
     // it, from block1's pre-split operand (groupnorm_silu_x3op, written once untimed).
+    // layers 6-8: the attention launches of the forward, timed the same way: 6 = level-0
+    // shifted STW attention (downs.0.1, in place on x), 7 = init_temporal_attn (x -> out),
+    // 8 = the TrajWarp cross-attention core over the pre-split cond-frame K / V (u12:719-773).
+    if (layer >= 6 && layer <= 8) {
+      const int C = h->cfg.dim;
+      double flop = 0;
+      std::function<void()> launch;
+      View x = h->alloc_cf(B, C, T, L, L), o = h->alloc_cf(B, C, T, L, L);
+      fill_normal(s, x.p, 1, (int)x.numel(), 17, 0, 0, 3);
+      const int hid = h->cfg.heads * h->cfg.dim_head;
+      if (layer == 6) {
+        REQUIRE(h->has("downs.0.1.fn.fn.attn.qkv.weight"), "bench layer 6: no level-0 STW layer");
+        const AttnGeom g = h->stw_geom(T, L, L, true);
+        const int N = g.ws0 * g.ws1 * g.ws2;
+        flop = (double)B * T * L * L * (2.0 * C * 3 * hid + 4.0 * N * hid + 2.0 * hid * C);
+        launch = [&] { h->stw("downs.0.1", x, true); };
+      } else if (layer == 7) {
+        REQUIRE(h->has("init_temporal_attn.fn.fn.fn.attn.to_qkv.weight"), "bench layer 7: no temporal layer");
+        flop = (double)B * T * L * L * (2.0 * C * 3 * hid + 4.0 * T * hid + 2.0 * hid * C);
+        launch = [&] { h->temporal("init_temporal_attn", x, o); };
+      } else {
+        REQUIRE(h->cfg.arch == EXTDM_ARCH_U12 && h->kv_split_ok(), "bench layer 8: no pre-split TrajWarp cross-attention");
+        const int fs = h->cfg.fea_size, Cf = h->cfg.fea_ch, nq = h->cfg.tp * fs * fs, nk = h->cfg.tc * fs * fs;
+        View fea = h->alloc_cf(B, Cf, T, fs, fs), q = h->alloc_cf(B, Cf, h->cfg.tp, fs, fs),
+             a = h->alloc_cf(B, Cf, h->cfg.tp, fs, fs);
+        fill_normal(s, fea.p, 1, (int)fea.numel(), 17, 0, 0, 4);
+        fill_normal(s, q.p, 1, (int)q.numel(), 17, 0, 0, 5);
+        h->trajwarp_kv(fea);
+        flop = (double)B * h->cfg.heads * 4.0 * nq * nk * (Cf / h->cfg.heads);
+        launch = [&, q, a, nq, nk, Cf] {
+          REQUIRE(cross_attention_x3p(s, q.p, h->kvp, a.p, B, Cf, h->cfg.heads, nq, nk), "bench layer 8: launch rejected");
+        };
+      }
+      launch();  // warm (packs the layer's weights and tables on first use)
+      hipEvent_t e0, e1;
+      HIPCHK(hipEventCreate(&e0));
+      HIPCHK(hipEventCreate(&e1));
+      HIPCHK(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; ++i) launch();
+      HIPCHK(hipEventRecord(e1, s));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      *ms_out = ms / iters;
+      *flops_out = flop;
+      return;
+    }
     static const char* names[] = {"init_conv.weight", "downs.0.0.block2.proj.weight", "downs.1.0.block2.proj.weight",
                                   "downs.2.0.block2.proj.weight", "ups.3.0.res_conv.weight",
                                   "downs.0.0.block2.proj.weight"};

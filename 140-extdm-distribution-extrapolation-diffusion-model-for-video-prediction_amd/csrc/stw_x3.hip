@@ -22,7 +22,10 @@
 // of two per matrix) are shared by the block's waves through a double-buffered
 // LDS-DMA ring, one barrier per unit.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 
 #include "kernels.h"
 
@@ -85,10 +88,14 @@ __device__ __forceinline__ Tok token_of(int tk, const AttnGeom& g, long st, int 
 // probabilities and scaled q / k / v here are products, whose two fp16 roundings hipcc
 // would otherwise lower differently (hi + lo off by an fp16 ulp in ~2^-13 of the values;
 // it made the reciprocal-multiply softmax fail at 2.7e-4).
-// CHECK: OR |v| >= 65504 (fp16 overflow of hi) into bad; the probabilities (in [0, 1])
-// skip it. Compiler-visible split2c rather than the split2 asm (kernels.h): these splits
-// read MFMA results and feed MFMAs, and only compiler-visible VALU gets its MFMA hazard
-// waits (4 VALU per pair; the per-element cvt / cvt-back / sub / pack took 8).
+// CHECK: OR |v| >= 65504 (fp16 overflow of hi) into bad. Only the normalised input is
+// checked value by value; the values split inside the unit loop (q, k, v, P, O) are
+// covered by one finite check of the token's projection accumulators in the epilogue:
+// an overflowing hi is +-inf and its lo the opposite infinity, so every MFMA sum the pair
+// enters holds inf - inf = NaN, and a NaN reaches the token's output through the scores
+// (max / exp2 / sum of its own query column) and PV. Compiler-visible split2m (3 VALU per
+// pair) rather than the split2 asm (kernels.h): these splits read MFMA results and feed
+// MFMAs, and only compiler-visible VALU gets its MFMA hazard waits.
 template <bool CHECK = true>
 __device__ __forceinline__ void split8(const float* v, h8& hi, h8& lo, int& bad) {
   float m = 0.f;
@@ -97,7 +104,7 @@ __device__ __forceinline__ void split8(const float* v, h8& hi, h8& lo, int& bad)
     const float w0 = split_src(v[e]), w1 = split_src(v[e + 1]);
     if (CHECK) m = fmaxf(fmaxf(m, fabsf(w0)), fabsf(w1));
     f16x2_t ph, pl;
-    split2c(w0, w1, ph, pl);
+    split2m(w0, w1, ph, pl);
     hi[e] = ph.x; hi[e + 1] = ph.y;
     lo[e] = pl.x; lo[e + 1] = pl.y;
   }
@@ -111,6 +118,19 @@ __device__ __forceinline__ f32x16 mma3(const h8& ah, const h8& al, const h8& bh,
   return c;
 }
 
+// Reductions across the two half-waves (lane ^ 32) without LDS: v_permlane32_swap of v
+// with itself leaves the partner's value in r[1] of the lower lanes and in r[0] of the
+// upper lanes (own value in the other), so r[0] op r[1] is the pair's result in both
+// halves (commutative: bitwise equal).
+__device__ __forceinline__ float xh_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xh_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 // Packed unit slice (halves): [q: C/16 frags][k: C/16][v: C/16][proj: C/32 tiles x 2 k-steps],
 // each frag = [hl][64 lanes][8].
 template <int C>
@@ -121,7 +141,15 @@ struct UnitLayout {
   static constexpr int HALVES = 3 * KS * FRAG + (C / 32) * 2 * FRAG;
 };
 
-template <int C, int MODE, int DH, int NW>
+// mbias: [npat][8 heads][32 queries][32 keys] fp32, the relative-position bias with the
+// masks folded in (build_mask_bias, runtime.cpp): -100 for a shifted window's region
+// mismatch (u12:414-436), -inf for keys past the window's N tokens and for another
+// pixel's frames (MODE 1). MODE 0 shifted layers carry 8 window classes (bit d: last
+// window along a shifted dim, where the region labels differ), the rest one. A lane's 16
+// score registers hold keys j = dof(r, h) = 8q + 4h + e (r = 4q + e): four 16-B rows of
+// its query's table row, loaded straight into the score accumulator that the QK^T
+// MFMAs then add to — no VALU for bias or masks.
+template <int C, int MODE, int DH, int NW, bool TILE>
 // x and out alias for the in-place STW layers (MODE 0): no __restrict__ on them.
 __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float* out,
                                                           long sb, long sc, long st, long osb, long osc, AttnGeom g,
@@ -131,11 +159,12 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
                                                           const _Float16* __restrict__ wpk,
                                                           const float* __restrict__ wsc,  // 2^-s: q, k, v, proj
                                                           const float* __restrict__ bp,
-                                                          const float* __restrict__ bias_dense, int bstride,
+                                                          const float* __restrict__ mbias, int npat,
                                                           const float* __restrict__ rcos,
                                                           const float* __restrict__ rsin, float q_scale,
                                                           int groups_per_sample, int total_groups,
-                                                          int* __restrict__ range_flag, int dbg) {
+                                                          int* __restrict__ range_flag, int dbg,
+                                                          long long* __restrict__ tstamp) {
   using UL = UnitLayout<C>;
   constexpr int KS = UL::KS;
   constexpr int UNITS = 8 * DH / 32;  // heads 8
@@ -146,13 +175,6 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int h = lane >> 5, lc = lane & 31;
-  const int gidx = blockIdx.x * NW + wave;
-  const bool active = gidx < total_groups;
-  const int b = active ? gidx / groups_per_sample : 0;
-  const int grp = active ? gidx % groups_per_sample : 0;
-  const float* xb = x + (long)b * sb;
-  float* ob = out + (long)b * osb;
   // Global traffic through buffer descriptors: a lane's 32-bit byte offset carries its token
   // (and channel half), the channel row goes into the wave-uniform soffset, and an invalid
   // token's offset lies past the extent (loads return 0, stores are dropped): no 64-bit
@@ -161,34 +183,114 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   constexpr int OOB = 0x40000000;
   const int x_bytes = (int)(((long)(C - 1) * sc + (long)g.D * st) * 4);
   const int o_bytes = (int)(((long)(C - 1) * osc + (long)g.D * st) * 4);
-  const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xb), 0, x_bytes, 0x00020000);
-  const auto rs_o = __builtin_amdgcn_make_buffer_rsrc(ob, 0, o_bytes, 0x00020000);
   const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(gamma), 0, C * 4, 0x00020000);
   const auto rs_lw = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(MODE == 1 ? ln_w : gamma), 0, C * 4, 0x00020000);
   const auto rs_lb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(MODE == 1 ? ln_b : gamma), 0, C * 4, 0x00020000);
+  const auto rs_mb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(mbias), 0, npat * 8 * 4096, 0x00020000);
   auto ldb = [](const __amdgpu_buffer_rsrc_t& r, int vo, int so) __attribute__((always_inline)) {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
   };
 
+
+  const float sq = wsc[0] * q_scale, sk = wsc[1], sv = wsc[2];
+  constexpr bool FOLD = C == 64;
+
+  const int h = lane >> 5, lc = lane & 31;
+  const int wg = blockIdx.x;
+  const int gidx = wg * NW + wave;
+  const bool active = gidx < total_groups;
+  const int b = active ? gidx / groups_per_sample : 0;
+  const int grp = active ? gidx % groups_per_sample : 0;
+  const float* xb = x + (long)b * sb;
+  float* ob = out + (long)b * osb;
+  // diagnostic builds only (EXTDM_X3_DBG & 32): s_memtime stamps per wave into tstamp
+  auto stamp = [&](int k) __attribute__((always_inline)) {
+    if (tstamp != nullptr && lane == 0) tstamp[(long)gidx * 24 + k] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
+  const auto rs_x = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xb), 0, x_bytes, 0x00020000);
+  const auto rs_o = __builtin_amdgcn_make_buffer_rsrc(ob, 0, o_bytes, 0x00020000);
+  // a unit's weight slice by LDS-DMA, UL::HALVES / 512 pieces of 1 KiB spread over the
+  // waves (a whole number each: static trip count)
+  static_assert((UL::HALVES / 512) % NW == 0, "unit slice pieces per wave");
   auto load_unit = [&](int u, _Float16* dst) {
     const _Float16* src = wpk + (long)u * UL::HALVES;
-    if (dbg & 1) {
-      for (int pc = wave; pc < UL::HALVES / 512; pc += NW)
-        *reinterpret_cast<h8*>(dst + pc * 512 + lane * 8) = *reinterpret_cast<const h8*>(src + pc * 512 + lane * 8);
-    } else {
-      for (int pc = wave; pc < UL::HALVES / 512; pc += NW)
-        __builtin_amdgcn_global_load_lds((const void*)(src + pc * 512 + lane * 8), (lds_ptr_t)(dst + pc * 512), 16, 0,
-                                         0);
-    }
-    if (dbg & 2) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+#pragma unroll
+    for (int i = 0; i < UL::HALVES / 512 / NW; ++i) {
+      const int pc = wave + i * NW;
+      __builtin_amdgcn_global_load_lds((const void*)(src + pc * 512 + lane * 8), (lds_ptr_t)(dst + pc * 512), 16, 0, 0);
     }
   };
   load_unit(0, wsm);
 
+  // ---- MODE 0 tile path (template TILE, host check attn_x3_tile_ok): the workgroup's 8 windows
+  // are one row of 2x4x4 windows across W = 32 (no padding), so together they read
+  // [C][2 frames x 4 rows][32] of x: 8 whole 128-B lines per channel. That tile is staged
+  // into LDS by LDS-DMA (one 1-KiB instruction per channel), the lanes read their token's
+  // channels from it, and the epilogue writes the layer output back into it and stores it
+  // as whole lines — 8 coalesced instructions per wave each way instead of 32 per-lane dword
+  // accesses that each touch 16 lines (the per-lane prologue / epilogue took ~30 % of the
+  // kernel, s_memtime stamps). The residual is read from the tile, not from HBM again.
+  // Layout [c][r = td*4 + th][32], the 16-B chunk q of row r stored at q ^ r: the 32 lanes of
+  // a half-wave (8 rows x 4 columns of one channel) read 32 distinct banks ((a/4) mod 32 for
+  // 4-B accesses; shifted windows straddle two chunks at complementary column offsets).
+  static_assert(!TILE || (MODE == 0 && C == 64 && NW == 8), "tile path: level-0 STW only");
+  float* const tileT = reinterpret_cast<float*>(wsm + 2 * UL::HALVES);
+  int trow[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // element offset of tile row r in a channel plane
+  if (TILE) {
+    const int grp0 = (wg * NW) % groups_per_sample;
+    const int nWw = g.Wp / g.ws2, nWh = g.Hp / g.ws1;
+    const int wh = (grp0 / nWw) % nWh, wd = grp0 / (nWw * nWh);
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+      trow[r] = ((wd * 2 + (r >> 2) + g.ss0) % g.Dp) * (int)st + ((wh * 4 + (r & 3) + g.ss1) % g.Hp) * 32;
+    const int r = lane >> 3, q = (lane & 7) ^ r;
+    int roff = trow[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) roff = r == i ? trow[i] : roff;
+#pragma unroll
+    for (int i = 0; i < C / NW; ++i) {
+      const int c = wave + i * NW;
+      __builtin_amdgcn_global_load_lds((const void*)(xb + (long)c * sc + roff + 4 * q), (lds_ptr_t)(tileT + c * 256),
+                                       16, 0, 0);
+    }
+    // the norm's gamma and the projection bias behind the tile (lanes 0-15 / 16-31 of wave 0)
+    if (wave == 0 && lane < 32)
+      __builtin_amdgcn_global_load_lds((const void*)(lane < 16 ? gamma + 4 * lane : bp + 4 * (lane - 16)),
+                                       (lds_ptr_t)(tileT + C * 256), 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  stamp(20);
+  // this lane's token in the tile (row lc >> 2, column 4 * window + tw + shift)
+  const int tcol = (4 * wave + (lane & 3) + g.ss2) & 31;
+  const int tidx = (lc >> 2) * 32 + (((tcol >> 2) ^ (lc >> 2)) << 2) + (tcol & 3);
+
+  // window class of the bias / mask table (MODE 0 shifted layers): bit d for the last
+  // window along a shifted dim d
+  int pat = 0;
+  if (TILE && npat > 1) {
+    // the workgroup's row of windows: ww = wave, (wd, wh) of its first window
+    const int grp0 = (wg * NW) % groups_per_sample;
+    const int nWd = g.Dp / g.ws0, nWh = g.Hp / g.ws1;
+    const int wh = (grp0 >> 3) % nWh, wd = (grp0 >> 3) / nWh;
+    pat = (g.ss0 && wd == nWd - 1 ? 1 : 0) | (g.ss1 && wh == nWh - 1 ? 2 : 0) | (g.ss2 && wave == 7 ? 4 : 0);
+  } else if (MODE == 0 && npat > 1) {
+    const int nWd = g.Dp / g.ws0, nWh = g.Hp / g.ws1, nWw = g.Wp / g.ws2;
+    const int ww = grp % nWw, wh = (grp / nWw) % nWh, wd = grp / (nWw * nWh);
+    pat = (g.ss0 && wd == nWd - 1 ? 1 : 0) | (g.ss1 && wh == nWh - 1 ? 2 : 0) | (g.ss2 && ww == nWw - 1 ? 4 : 0);
+  }
+  // (wave-uniform: readfirstlane keeps the soffset in an SGPR — hipcc's divergence analysis
+  // does not see through the window decomposition and would waterfall the loads)
+  const int mb_lane = (lc * 32 + 4 * h) * 4, mb_wave = __builtin_amdgcn_readfirstlane(pat * 8 * 4096);
+
   // ---- 1. normalisation into register fragments ----
-  const Tok me = token_of<MODE>(lc, g, st, grp);
+  Tok me;
+  if (TILE) {  // every token of a tile window exists and lies inside the volume
+    me.pos = 0; me.valid = 1; me.exists = 1; me.lab = 0; me.rpos = lc;
+  } else {
+    me = token_of<MODE>(lc, g, st, grp);
+  }
   const bool tok_ok = active && me.valid;
   const int vpro = tok_ok ? (int)((8 * h * sc + me.pos) * 4) : OOB;  // channel 8h + (16k + e)
   int bad = 0;
@@ -201,78 +303,63 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     for (int k = 0; k < KS; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int c = 16 * k + 8 * h + e;
-        // dbg & 4 (timing only): no x loads
-        xv[k][e] = (dbg & 4) ? (tok_ok ? (float)(c ^ lane) * 0.01f : 0.f)
-                             : ldb(rs_x, vpro, (int)((16 * k + e) * sc * 4));
+        xv[k][e] = TILE ? tileT[(16 * k + 8 * h + e) * 256 + tidx]
+                                  : ldb(rs_x, vpro, (int)((16 * k + e) * sc * 4));
         s += xv[k][e];
       }
-    s += __shfl_xor(s, 32);
+    s = xh_sum(s);
     m1 = s / C;
     float v = 0.f;
 #pragma unroll
     for (int k = 0; k < KS; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) { const float d = xv[k][e] - m1; v += d * d; }
-    v += __shfl_xor(v, 32);
+    v = xh_sum(v);
+    stamp(21);
     den1 = sqrtf(v / C + 1e-5f);
     // one reciprocal instead of a division per element (~10 VALU each, in the prologue and
     // MODE 1's epilogue): the product differs from the quotient by at most an ulp
     rden1 = 1.f / den1;
+    // padded tokens (x loads 0 there) normalise to 0 through a 0 factor, not a select:
+    // with a select hipcc sank each gamma load into a branch of its own, waited for it
+    // there and so serialised 32 L2 round trips per wave
+    const float vm = me.valid ? 1.f : 0.f;
     if (MODE == 0) {
+      const float rv = rden1 * vm;
 #pragma unroll
       for (int k = 0; k < KS; ++k)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int c = 16 * k + 8 * h + e;
-          xv[k][e] = me.valid ? (xv[k][e] - m1) * rden1 * ldb(rs_g, 32 * h, (16 * k + e) * 4) : 0.f;
-        }
+        for (int e = 0; e < 8; ++e)
+          xv[k][e] = (xv[k][e] - m1) * rv * (TILE ? tileT[C * 256 + 16 * k + 8 * h + e] : ldb(rs_g, 32 * h, (16 * k + e) * 4));
     } else {
       float s2 = 0.f;
 #pragma unroll
       for (int k = 0; k < KS; ++k)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const int c = 16 * k + 8 * h + e;
           xv[k][e] = (xv[k][e] - m1) * rden1 * ldb(rs_g, 32 * h, (16 * k + e) * 4);
           s2 += xv[k][e];
         }
-      s2 += __shfl_xor(s2, 32);
+      s2 = xh_sum(s2);
       const float m2 = s2 / C;
       float v2 = 0.f;
 #pragma unroll
       for (int k = 0; k < KS; ++k)
 #pragma unroll
         for (int e = 0; e < 8; ++e) { const float d = xv[k][e] - m2; v2 += d * d; }
-      v2 += __shfl_xor(v2, 32);
+      v2 = xh_sum(v2);
       const float rstd2 = 1.0f / sqrtf(v2 / C + 1e-5f);
 #pragma unroll
       for (int k = 0; k < KS; ++k)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int c = 16 * k + 8 * h + e;
-          xv[k][e] = me.valid ? (xv[k][e] - m2) * rstd2 * ldb(rs_lw, 32 * h, (16 * k + e) * 4) +
-                                    ldb(rs_lb, 32 * h, (16 * k + e) * 4)
-                              : 0.f;
-        }
+        for (int e = 0; e < 8; ++e)
+          xv[k][e] = ((xv[k][e] - m2) * rstd2 * ldb(rs_lw, 32 * h, (16 * k + e) * 4) +
+                      ldb(rs_lb, 32 * h, (16 * k + e) * 4)) * vm;
     }
 #pragma unroll
     for (int k = 0; k < KS; ++k) split8(xv[k], xh[k], xl[k], bad);
   }
-  // key-side token descriptors for the 16 keys j = dof(r, h) this lane's scores hold
-  const bool shifted = MODE == 0 && (g.ss0 | g.ss1 | g.ss2) != 0;
-  const int desc = (me.lab & 0xFFFF) | (me.exists << 16);
-  // The keys j = dof(r, h) of this lane's score registers do not depend on the unit:
-  // their masks are computed once (bit r), and their positions are known in closed
-  // form, so the bias loads carry no shuffle dependency and issue early.
-  unsigned kmis = 0, kgone = 0;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int dj = __shfl(desc, dof(r, h));
-    kmis |= (unsigned)((dj & 0xFFFF) != me.lab) << r;
-    kgone |= (unsigned)(!((dj >> 16) & 1)) << r;
-  }
-  const int kper = g.D <= 16 ? 16 : 32;
+  stamp(22);
 
   f32x16 pacc[CT];
 #pragma unroll
@@ -280,12 +367,10 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 #pragma unroll
     for (int r = 0; r < 16; ++r) pacc[i][r] = 0.f;
 
-  const float sq = wsc[0] * q_scale, sk = wsc[1], sv = wsc[2];
   // RoPE factors of this lane's (token, dim pair) registers, the same for every unit (with
-  // the q / k scales folded in when FOLD)
-  // folded at C = 64 only: at C = 128 (one wave per SIMD) the 16 extra live registers
-  // cost 20 % (interleaved A/B)
-  constexpr bool FOLD = C == 64;
+  // the q / k scales folded in when FOLD); reloaded per group rather than kept live through
+  // the prologue. Folded at C = 64 only: at C = 128 (one wave per SIMD) the 16 extra live
+  // registers cost 20 % (interleaved A/B)
   float rcq[8], rsq[8], rck[8], rsk[8];
 #pragma unroll
   for (int r = 0; r < 16; r += 2) {
@@ -294,30 +379,44 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     rcq[r >> 1] = FOLD ? c * sq : c; rsq[r >> 1] = FOLD ? sn * sq : sn;
     rck[r >> 1] = FOLD ? c * sk : c; rsk[r >> 1] = FOLD ? sn * sk : sn;
   }
-  for (int u = 0; u < UNITS; ++u) {
-    _Float16* W = wsm + (u & 1) * UL::HALVES;
-    // unit u's slice has landed in every wave's pieces: LDS-DMA completion is tracked by
-    // the issuing wave's vmcnt only, so each wave drains it before the barrier
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // ... and slot (u+1)&1 is free
-    if (u + 1 < UNITS) load_unit(u + 1, wsm + ((u + 1) & 1) * UL::HALVES);
-    if (!active) continue;
-    // ---- 2a. Q^T, K^T (rows = dims, lane = token), V (rows = tokens, lane = dim) ----
-    f32x16 q, k, v;
+
+  // ---- 2. per unit of 32 qkv rows ----
+  // Q^T, K^T (rows = dims, lane = token) from the unit slice W
+  auto qk_mfma = [&](const _Float16* W, f32x16& q, f32x16& k) __attribute__((always_inline)) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { q[r] = 0.f; k[r] = 0.f; v[r] = 0.f; }
+    for (int r = 0; r < 16; ++r) { q[r] = 0.f; k[r] = 0.f; }
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const _Float16* fq = W + UL::Q + s * UL::FRAG + lane * 8;
       const _Float16* fk = W + UL::K + s * UL::FRAG + lane * 8;
-      const _Float16* fv = W + UL::V + s * UL::FRAG + lane * 8;
-      const h8 qh = *reinterpret_cast<const h8*>(fq), ql = *reinterpret_cast<const h8*>(fq + 512);
-      const h8 kh = *reinterpret_cast<const h8*>(fk), kl = *reinterpret_cast<const h8*>(fk + 512);
-      const h8 vh = *reinterpret_cast<const h8*>(fv), vl = *reinterpret_cast<const h8*>(fv + 512);
-      q = mma3(qh, ql, xh[s], xl[s], q);
-      k = mma3(kh, kl, xh[s], xl[s], k);
-      v = mma3(xh[s], xl[s], vh, vl, v);
+      q = mma3(*reinterpret_cast<const h8*>(fq), *reinterpret_cast<const h8*>(fq + 512), xh[s], xl[s], q);
+      k = mma3(*reinterpret_cast<const h8*>(fk), *reinterpret_cast<const h8*>(fk + 512), xh[s], xl[s], k);
     }
+  };
+  // V (rows = tokens, lane = dim)
+  auto v_mfma = [&](const _Float16* W, f32x16& v) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const _Float16* fv = W + UL::V + s * UL::FRAG + lane * 8;
+      v = mma3(xh[s], xl[s], *reinterpret_cast<const h8*>(fv), *reinterpret_cast<const h8*>(fv + 512), v);
+    }
+  };
+  // the bias / mask rows of unit u's heads (straight into the score accumulators)
+  auto load_bias = [&](int u, f32x16* bia) __attribute__((always_inline)) {
+#pragma unroll
+    for (int hh = 0; hh < HPU; ++hh)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rs_mb, mb_lane + 32 * q, mb_wave + (u * HPU + hh) * 4096, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bia[hh][4 * q + e] = __uint_as_float(v4[e]);
+      }
+  };
+  // scale + RoPE of q, k; the unit's heads: S^T = bias + K Q^T (rows = keys j, lane =
+  // query i), softmax, O^T = V^T P^T
+  auto attend = [&](f32x16& q, f32x16& k, const f32x16& v, const f32x16* bia) __attribute__((always_inline)) {
     // scale, RoPE on (d, d+1) = registers (r, r+1); d = dof(r, h) within the head
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
@@ -331,47 +430,29 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       k[r] = fmaf(k0, rck[r >> 1], -(k1 * rsk[r >> 1]));
       k[r + 1] = fmaf(k1, rck[r >> 1], k0 * rsk[r >> 1]);
     }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] *= sv;
     h8 qf[2][2], kf[2][2], vf[2][2];  // [k-step][hi|lo]
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float tq[8], tk[8], tv[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { tq[e] = q[8 * s + e]; tk[e] = k[8 * s + e]; tv[e] = v[8 * s + e]; }
-      split8(tq, qf[s][0], qf[s][1], bad);
-      split8(tk, kf[s][0], kf[s][1], bad);
-      split8(tv, vf[s][0], vf[s][1], bad);
+      for (int e = 0; e < 8; ++e) { tq[e] = q[8 * s + e]; tk[e] = k[8 * s + e]; tv[e] = v[8 * s + e] * sv; }
+      split8<false>(tq, qf[s][0], qf[s][1], bad);
+      split8<false>(tk, kf[s][0], kf[s][1], bad);
+      split8<false>(tv, vf[s][0], vf[s][1], bad);
     }
-    // ---- 2b. per head: S^T = K Q^T (rows = keys j, lane = query i), softmax, O^T += V^T P^T ----
     f32x16 o;
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[r] = 0.f;
 #pragma unroll
     for (int hh = 0; hh < HPU; ++hh) {
-      const int head = u * HPU + hh;
-      f32x16 sc_;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sc_[r] = 0.f;
+      f32x16 sc_ = bia[hh];
 #pragma unroll
       for (int s = 0; s < 2; ++s)
         if (HPU == 1 || s == hh) sc_ = mma3(kf[s][0], kf[s][1], qf[s][0], qf[s][1], sc_);
-      const float* bd = bias_dense + ((long)head * bstride + me.rpos) * bstride;
       float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int j = dof(r, h);
-        float s_ = sc_[r] + bd[MODE == 0 ? j : j % kper];
-        if (MODE == 0) {
-          if (shifted && ((kmis >> r) & 1)) s_ += -100.f;
-        } else {
-          if ((kmis >> r) & 1) s_ = -INFINITY;
-        }
-        if ((kgone >> r) & 1) s_ = -INFINITY;
-        sc_[r] = s_;
-        mx = fmaxf(mx, s_);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc_[r]);
+      mx = xh_max(mx);
       // exp(s - mx) as v_exp_f32 (2^x) of fma(s, log2 e, -mx log2 e): masked -inf -> 0
       const float mxl = mx * 1.44269504088896341f;
       float sum = 0.f;
@@ -380,7 +461,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
         sc_[r] = __builtin_amdgcn_exp2f(fmaf(sc_[r], 1.44269504088896341f, -mxl));
         sum += sc_[r];
       }
-      sum += __shfl_xor(sum, 32);
+      sum = xh_sum(sum);
       const float inv = 1.f / sum;
 #pragma unroll
       for (int r = 0; r < 16; ++r) sc_[r] *= inv;
@@ -401,20 +482,61 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
         o = mma3(ah, al, ph, pl, o);
       }
     }
-    // ---- 2c. projection: Y[c][i] += sum_dd Wp[c][u*32 + dd] O^T[dd][i] ----
+    return o;
+  };
+  // projection: Y[c][i] += sum_dd Wp[c][u*32 + dd] O^T[dd][i]
+  auto proj = [&](const _Float16* W, const f32x16& o) __attribute__((always_inline)) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float to[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) to[e] = o[8 * s + e];
       h8 oh, ol;
-      split8(to, oh, ol, bad);
+      split8<false>(to, oh, ol, bad);
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         const _Float16* fp = W + UL::P + (ct * 2 + s) * UL::FRAG + lane * 8;
         pacc[ct] = mma3(*reinterpret_cast<const h8*>(fp), *reinterpret_cast<const h8*>(fp + 512), oh, ol, pacc[ct]);
       }
     }
+  };
+  // unit u's slice has landed in every wave's pieces: LDS-DMA completion is tracked by
+  // the issuing wave's vmcnt only, so each wave drains it before the barrier
+  auto unit_barrier = [&](int u) __attribute__((always_inline)) {
+    stamp(2 + 2 * u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    stamp(3 + 2 * u);
+  };
+  stamp(1);
+  if (dbg & 16) {
+    // timing only: no unit loop (prologue + epilogue cost)
+  } else {
+    for (int u = 0; u < UNITS; ++u) {
+      _Float16* W = wsm + (u & 1) * UL::HALVES;
+      unit_barrier(u);  // ... and slot (u+1)&1 is free
+      // the unit's bias / mask rows, issued ahead of the next unit's weight DMA: vmcnt
+      // counts in issue order, so waiting for them does not wait for the DMA
+      f32x16 bia[HPU];
+      load_bias(u, bia);
+      if (u + 1 < UNITS) load_unit(u + 1, wsm + ((u + 1) & 1) * UL::HALVES);
+      if (!active) continue;
+      f32x16 q, k, v;
+      qk_mfma(W, q, k);
+      v_mfma(W, v);
+      const f32x16 o = attend(q, k, v, bia);
+      proj(W, o);
+    }
+  }
+  stamp(18);
+  // the loop's splits: one finite check of the token's accumulators (see split8)
+  {
+    float chk = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) chk += pacc[ct][r];
+    bad |= tok_ok && !__builtin_isfinite(chk);
   }
   if (bad) atomicOr(range_flag, 2);
   // MODE 1 with 2-pixel groups: a lane's token is (pixel, frame), so a direct store touches
@@ -443,89 +565,162 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
         }
     }
     __syncthreads();
-    if (!active) return;
-    const int hw0 = (blockIdx.x * NW) % groups_per_sample * 2;
-    float* o0 = ob + hw0;
-    for (int i = tid; i < C * g.D * 4; i += NW * 64) {
-      const int q = i & 3, ctr = i >> 2;
-      const int t = ctr % g.D, c = ctr / g.D;
-      const float4 v = *reinterpret_cast<const float4*>(T + c * CS + t * RS + 4 * q);
-      *reinterpret_cast<float4*>(o0 + (long)c * osc + (long)t * st + 4 * q) = v;
+    if (active) {
+      const int hw0 = (wg * NW) % groups_per_sample * 2;
+      float* o0 = ob + hw0;
+      for (int i = tid; i < C * g.D * 4; i += NW * 64) {
+        const int q = i & 3, ctr = i >> 2;
+        const int t = ctr % g.D, c = ctr / g.D;
+        const float4 v = *reinterpret_cast<const float4*>(T + c * CS + t * RS + 4 * q);
+        *reinterpret_cast<float4*>(o0 + (long)c * osc + (long)t * st + 4 * q) = v;
+      }
     }
-    return;
-  }
-  if (!active || !me.valid) return;
-  if (dbg & 8) {  // timing only: no epilogue loads / stores (one store keeps the work live)
-    float acc = 0.f;
+  } else if (active && me.valid) {
+    if (dbg & 8) {  // timing only: no epilogue loads / stores (one store keeps the work live)
+      float acc = 0.f;
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
+      for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc += pacc[ct][r];
-    if (acc == 12345.f) ob[me.pos] = acc;
-    return;
+        for (int r = 0; r < 16; ++r) acc += pacc[ct][r];
+      if (acc == 12345.f) ob[me.pos] = acc;
+    } else {
+      // ---- 3. bias + residual, write back ----
+      // row c = cu + 4h of register r: the lane offset carries 4h, the soffset cu
+      const float spj = wsc[3];
+      const int vex = (int)((4 * h * sc + me.pos) * 4), veo = (int)((4 * h * osc + me.pos) * 4);
+      const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(MODE == 0 ? bp : gamma), 0, C * 4, 0x00020000);
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int cu = ct * 32 + (r & 3) + 8 * (r >> 2);
+          // MODE 0: proj bias; MODE 1: gamma
+          const float pb = TILE ? tileT[C * 256 + 64 + cu + 4 * h] : ldb(rs_b, 16 * h, cu * 4);
+          const float y = pacc[ct][r] * spj;
+          if (TILE) {
+            // residual from the tile, the result back into it (each (channel, token) is one lane's)
+            float* tp = tileT + (cu + 4 * h) * 256 + tidx;
+            *tp = (y + pb) + *tp;
+          } else {
+            const float xv = ldb(rs_x, vex, (int)(cu * sc * 4));
+            float res;
+            if (MODE == 0) res = (y + pb) + xv;
+            else res = y + (xv + (xv - m1) * rden1 * pb);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(res), rs_o, veo, (int)(cu * osc * 4), 0);
+          }
+        }
+      }
+    }
+    stamp(19);
   }
+  if (TILE) {
+    // the tile leaves as whole 128-B lines: chunk id -> (channel, row, stored chunk), its
+    // global chunk undoes the row's swizzle
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < C * 64 / (NW * 64); ++j) {
+      const int id = tid + j * NW * 64;
+      const int c = id >> 6, r = (id >> 3) & 7, qs = id & 7;
+      int roff = trow[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i) roff = r == i ? trow[i] : roff;
+      const float4 v = *reinterpret_cast<const float4*>(tileT + c * 256 + r * 32 + qs * 4);
+      *reinterpret_cast<float4*>(ob + (long)c * osc + roff + 4 * (qs ^ r)) = v;
+    }
+  }
+}
 
-  // ---- 3. bias + residual, write back ----
-  // row c = cu + 4h of register r: the lane offset carries 4h, the soffset cu
-  const float spj = wsc[3];
-  const int vex = (int)((4 * h * sc + me.pos) * 4), veo = (int)((4 * h * osc + me.pos) * 4);
-  const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(MODE == 0 ? bp : gamma), 0, C * 4, 0x00020000);
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int cu = ct * 32 + (r & 3) + 8 * (r >> 2);
-      const float xv = ldb(rs_x, vex, (int)(cu * sc * 4));
-      const float pb = ldb(rs_b, 16 * h, cu * 4);  // MODE 0: proj bias; MODE 1: gamma
-      const float y = pacc[ct][r] * spj;
-      float res;
-      if (MODE == 0) res = (y + pb) + xv;
-      else res = y + (xv + (xv - m1) * rden1 * pb);
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(res), rs_o, veo, (int)(cu * osc * 4), 0);
-    }
-  }
+// The MODE 0 tile path (kernel header, "tile path"): 2x4x4 windows over W = 32 without
+// padding, so that a workgroup's 8 windows are one row of windows; 16-B aligned rows;
+// in place (x and out the same view).
+bool attn_x3_tile_ok(const View& x, const View& out, const AttnGeom& g, int groups) {
+  static const bool off = [] { const char* v = getenv("EXTDM_X3_NO_TILE"); return v && v[0] && v[0] != '0'; }();
+  return !off && g.mode == 0 && g.ws0 == 2 && g.ws1 == 4 && g.ws2 == 4 && g.W == 32 && g.Wp == 32 && g.H == g.Hp &&
+         g.D == g.Dp && groups % 8 == 0 && x.p == out.p && x.sc == out.sc && x.sb == out.sb && x.st == out.st &&
+         x.st == (long)x.H * x.W && x.sc % 4 == 0 && x.sb % 4 == 0 && ((uintptr_t)x.p & 15) == 0;
 }
 
 template <int C, int MODE, int DH, int NW>
 void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int groups, const float* gamma,
                const float* lw, const float* lb, const void* wpk, const float* wsc, const float* bp,
-               const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale) {
+               const float* mbias, int npat, const float* rcos, const float* rsin, float q_scale) {
   static const int dbg = [] { const char* v = getenv("EXTDM_X3_DBG"); return v ? atoi(v) : 0; }();
   // MODE 1 at C = 64, 8 waves: the epilogue's [C][16 frames][16 px] staging tile (rows of
   // 20, channels of 328 floats) reuses the ring
   const size_t ring = (size_t)2 * UnitLayout<C>::HALVES * sizeof(_Float16);
-  const size_t lds = (MODE == 1 && C == 64 && NW == 8) ? std::max(ring, (size_t)C * 328 * sizeof(float)) : ring;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW>),
+  const bool tile = MODE == 0 && C == 64 && NW == 8 && attn_x3_tile_ok(x, out, g, groups);
+  size_t lds = (MODE == 1 && C == 64 && NW == 8) ? std::max(ring, (size_t)C * 328 * sizeof(float)) : ring;
+  if (tile) lds = ring + ((size_t)C * 8 * 32 + 2 * 64) * sizeof(float);
+  // per device, once: the dynamic-LDS limit
+  static std::once_flag once[64];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::call_once(once[dev & 63], [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW, false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+    if (MODE == 0 && C == 64 && NW == 8)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW, MODE == 0 && C == 64 && NW == 8>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
   const int total = x.B * groups;
-  hipLaunchKernelGGL((attn_x3_kernel<C, MODE, DH, NW>), dim3((total + NW - 1) / NW), dim3(NW * 64), lds, s, x.p,
-                     out.p, x.sb, x.sc, x.st, out.sb, out.sc, g, gamma, lw, lb,
-                     reinterpret_cast<const _Float16*>(wpk), wsc, bp, bias_dense, bstride, rcos, rsin, q_scale, groups,
-                     total, x3_range_ptr(), dbg);
+  const int grid = (total + NW - 1) / NW;
+  long long* ts = nullptr;
+  if (dbg & 32) {  // diagnostic: per-wave s_memtime stamps, mean phase durations to stderr
+    (void)hipMalloc(&ts, (size_t)total * 24 * sizeof(long long));
+    (void)hipMemsetAsync(ts, 0, (size_t)total * 24 * sizeof(long long), s);
+  }
+  constexpr bool TILE_OK = MODE == 0 && C == 64 && NW == 8;
+  auto kern = tile ? &attn_x3_kernel<C, MODE, DH, NW, TILE_OK> : &attn_x3_kernel<C, MODE, DH, NW, false>;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, s, x.p, out.p, x.sb, x.sc, x.st, out.sb, out.sc, g, gamma,
+                     lw, lb, reinterpret_cast<const _Float16*>(wpk), wsc, bp, mbias, npat, rcos, rsin, q_scale, groups,
+                     total, x3_range_ptr(), dbg, ts);
+  if (ts) {
+    std::vector<long long> h((size_t)total * 24);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), ts, h.size() * sizeof(long long), hipMemcpyDeviceToHost);
+    (void)hipFree(ts);
+    double acc[24] = {0};
+    long n = 0;
+    for (int w = 0; w < total; ++w) {
+      const long long* t = &h[(size_t)w * 24];
+      if (t[0] == 0 || t[19] == 0) continue;
+      ++n;
+      for (int k = 1; k < 20; ++k) acc[k] += (double)(t[k] - t[k - 1]);
+    }
+    fprintf(stderr, "attn_x3<C=%d,MODE=%d,DH=%d,NW=%d> stamps over %ld waves (cycles): prologue %.0f", C, MODE, DH, NW, n,
+            acc[1] / n);
+    for (int u = 0; u < 8; ++u) fprintf(stderr, " | u%d wait %.0f body %.0f", u, acc[3 + 2 * u] / n, acc[4 + 2 * u] / n);
+    fprintf(stderr, " | tail %.0f epilogue %.0f", acc[18] / n, acc[19] / n);
+    double p[4] = {0, 0, 0, 0};  // prologue: tile wait / LN statistics / normalise + split / rest
+    for (int w = 0; w < total; ++w) {
+      const long long* t = &h[(size_t)w * 24];
+      if (t[0] == 0 || t[19] == 0 || t[20] == 0) continue;
+      p[0] += (double)(t[20] - t[0]); p[1] += (double)(t[21] - t[20]); p[2] += (double)(t[22] - t[21]);
+      p[3] += (double)(t[1] - t[22]);
+    }
+    fprintf(stderr, " || prologue: tile-wait %.0f stats %.0f norm+split %.0f rope+rest %.0f\n", p[0] / n, p[1] / n,
+            p[2] / n, p[3] / n);
+  }
 }
 
 template <int C, int MODE, int DH>
 void launch(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int groups, const float* gamma,
             const float* lw, const float* lb, const void* wpk, const float* wsc, const float* bp,
-            const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale) {
+            const float* mbias, int npat, const float* rcos, const float* rsin, float q_scale) {
   static const int nw = [] { const char* v = getenv("EXTDM_X3_ATTN_NW"); return v ? atoi(v) : 0; }();
   // C = 128 needs > 256 VGPRs: one wave per SIMD
   if (C == 64 && nw != 4)
-    launch_nw<C, MODE, DH, 8>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, bias_dense, bstride, rcos, rsin, q_scale);
+    launch_nw<C, MODE, DH, 8>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
   else
-    launch_nw<C, MODE, DH, 4>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, bias_dense, bstride, rcos, rsin, q_scale);
+    launch_nw<C, MODE, DH, 4>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
 }
 
 template <int MODE, int DH>
 bool dispatch_c(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int groups, const float* gamma,
                 const float* lw, const float* lb, const void* wpk, const float* wsc, const float* bp,
-                const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale) {
-  if (x.C == 64) launch<64, MODE, DH>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, bias_dense, bstride, rcos, rsin, q_scale);
-  else if (x.C == 128) launch<128, MODE, DH>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, bias_dense, bstride, rcos, rsin, q_scale);
+                const float* mbias, int npat, const float* rcos, const float* rsin, float q_scale) {
+  if (x.C == 64) launch<64, MODE, DH>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
+  else if (x.C == 128) launch<128, MODE, DH>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
   else return false;
   return true;
 }
@@ -548,29 +743,30 @@ static bool extent_ok(const View& v, const AttnGeom& g) {
 }
 
 bool stw_x3(hipStream_t s, const View& x, const AttnGeom& g, int heads, int dim_head, const float* gamma,
-            const void* wpk, const float* wsc, const float* bp, const float* bias_dense, int bstride,
+            const void* wpk, const float* wsc, const float* bp, const float* mbias, int npat,
             const float* rcos, const float* rsin, float q_scale) {
   const int N = g.ws0 * g.ws1 * g.ws2;
   if (!attn_x3_supported(x.C, N, dim_head, heads) || !extent_ok(x, g)) return false;
   const int groups = (g.Dp / g.ws0) * (g.Hp / g.ws1) * (g.Wp / g.ws2);
   if (dim_head == 32)
-    return dispatch_c<0, 32>(s, x, x, g, groups, gamma, nullptr, nullptr, wpk, wsc, bp, bias_dense, bstride, rcos,
+    return dispatch_c<0, 32>(s, x, x, g, groups, gamma, nullptr, nullptr, wpk, wsc, bp, mbias, npat, rcos,
                              rsin, q_scale);
-  return dispatch_c<0, 16>(s, x, x, g, groups, gamma, nullptr, nullptr, wpk, wsc, bp, bias_dense, bstride, rcos, rsin,
+  return dispatch_c<0, 16>(s, x, x, g, groups, gamma, nullptr, nullptr, wpk, wsc, bp, mbias, npat, rcos, rsin,
                            q_scale);
 }
 
 bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, int dim_head,
                  const float* gamma, const float* ln_w, const float* ln_b, const void* wpk, const float* wsc,
-                 const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale) {
+                 const float* mbias, const float* rcos, const float* rsin, float q_scale) {
+  const int npat = 1;
   if (!attn_x3_supported(x.C, g.D, dim_head, heads) || g.D > 32 || !extent_ok(x, g) || !extent_ok(out, g)) return false;
   if (out.sc != x.sc || out.st != x.st) return false;
   const int ppb = g.D <= 16 ? 2 : 1;
   const int groups = (g.H * g.W + ppb - 1) / ppb;
   if (dim_head == 32)
-    return dispatch_c<1, 32>(s, x, out, g, groups, gamma, ln_w, ln_b, wpk, wsc, nullptr, bias_dense, bstride, rcos,
+    return dispatch_c<1, 32>(s, x, out, g, groups, gamma, ln_w, ln_b, wpk, wsc, nullptr, mbias, npat, rcos,
                              rsin, q_scale);
-  return dispatch_c<1, 16>(s, x, out, g, groups, gamma, ln_w, ln_b, wpk, wsc, nullptr, bias_dense, bstride, rcos, rsin,
+  return dispatch_c<1, 16>(s, x, out, g, groups, gamma, ln_w, ln_b, wpk, wsc, nullptr, mbias, npat, rcos, rsin,
                            q_scale);
 }
 

@@ -29,11 +29,18 @@ def shard(global_batch, world, rank):
     return start, count
 
 
+def _host_staged():
+    # gloo collectives take host tensors (the one-GPU rehearsal of the rank path)
+    return dist.is_initialized() and dist.get_backend() == 'gloo'
+
+
 def gather_shards(local, global_batch, world):
     """All-gather the ranks' slices (dim 0) into the global batch in rank order.
     Uneven slices are padded to the largest one for the collective."""
     if world == 1:
         return local
+    if _host_staged() and local.device.type != 'cpu':
+        return gather_shards(local.cpu(), global_batch, world).to(local.device)
     cap = -(-global_batch // world)
     pad = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[:local.shape[0]] = local
@@ -50,6 +57,6 @@ def max_over_ranks(value, device=None):
     """The slowest rank's wall time (bench.py's timing rule)."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64, device=None if _host_staged() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -46,16 +46,23 @@ def frame_metrics(videos1, videos2, layout='ntchw'):
     return psnr, ssim
 
 
+def _as_chw(img):
+    # the reference also takes a 2-D [h, w] image (calculate_ssim.py:31-32)
+    return img[None] if img.dim() == 2 else img
+
+
 def img_psnr(img1, img2):
-    """metrics/calculate_psnr.py:6-15 for one [c, h, w] image."""
-    return float(frame_metrics(img1[None, None], img2[None, None])[0][0, 0])
+    """metrics/calculate_psnr.py:6-15 for one [c, h, w] (or [h, w]) image."""
+    return float(frame_metrics(_as_chw(img1)[None, None], _as_chw(img2)[None, None])[0][0, 0])
 
 
 def calculate_ssim_function(img1, img2):
-    """metrics/calculate_ssim.py:26-41 for one [c, h, w] image (c in {1, 3})."""
+    """metrics/calculate_ssim.py:26-41 for one [c, h, w] (c in {1, 3}) or [h, w] image."""
     if img1.shape != img2.shape:
         raise ValueError('Input images must have the same dimensions.')
-    return float(frame_metrics(img1[None, None], img2[None, None])[1][0, 0])
+    if img1.dim() not in (2, 3):
+        raise ValueError('Wrong input image dimensions.')
+    return float(frame_metrics(_as_chw(img1)[None, None], _as_chw(img2)[None, None])[1][0, 0])
 
 
 def _per_frame_summary(vals, name, shape):
@@ -152,7 +159,9 @@ def eval_metrics(origin_videos, result_videos, cond_frames, origin_feats=None, r
     calculate_ssim2), summarised by metric_stuff. With video features given (origin [b, d],
     result [b * n, d]; the reference's I3D features, not shipped with it), the best sample
     per clip by feature L1 (valid.py:234-240) and its frechet_distance to the originals
-    ('fvd_best'). LPIPS needs network weights the reference does not ship: not computed."""
+    ('fvd_best'), and one frechet_distance per sample trajectory summarised by metric_stuff
+    ('fvd_traj_mean' / '_std' / '_conf95', valid.py:207-213). LPIPS needs network weights
+    the reference does not ship: not computed."""
     psnr_list, ssim_list = best_of_n(origin_videos, result_videos, cond_frames)
     avg_psnr, std_psnr, conf95_psnr = metric_stuff(np.array(psnr_list))
     avg_ssim, std_ssim, conf95_ssim = metric_stuff(np.array(ssim_list))
@@ -165,4 +174,7 @@ def eval_metrics(origin_videos, result_videos, cond_frames, origin_feats=None, r
         best = rf[np.arange(len(idx)), idx]
         out['fvd_best'] = frechet_distance(np.asarray(origin_feats), best)
         out['selected_index'] = idx
+        # per trajectory: the features of every clip's traj-th sample (valid.py:207-209)
+        fvd_list = [frechet_distance(np.asarray(origin_feats), rf[:, traj]) for traj in range(n)]
+        out['fvd_traj_mean'], out['fvd_traj_std'], out['fvd_traj_conf95'] = metric_stuff(np.array(fvd_list))
     return out

@@ -110,18 +110,30 @@ class Unet3D(nn.Module):
             raise AssertionError(f'wo_ref concatenates cond_fea at the latent size {self.ucfg.latent}, got {n}')
         self.ucfg = dataclasses.replace(self.ucfg, fea_size=n)
 
+    # native handles kept per (fea_size, ...) key: inputs alternating between cond_fea sizes
+    # reuse their handles instead of re-packing every weight on each switch
+    _NATIVE_CACHE = 4
+
     def native(self, timesteps_buffers, max_batch, device_index):
         ver = (self._state_version(), id(timesteps_buffers), max_batch, device_index, self.precision,
                self.ucfg.fea_size)
-        if self._native is None or self._native_version != ver:
+        cache = self.__dict__.setdefault('_natives', {})
+        h = cache.get(ver)
+        if h is None:
+            # weights or schedule changed: handles of the old state are stale
+            for k in [k for k in cache if k[:2] != ver[:2]]:
+                del cache[k]
+            while len(cache) >= self._NATIVE_CACHE:
+                del cache[next(iter(cache))]
             h = _lib.Handle(self.ucfg, int(timesteps_buffers['betas'].shape[0]), max_batch, device_index,
                             precision=self.precision)
             sd = {k: v for k, v in self.state_dict().items()}
             sd.update(timesteps_buffers)
             h.load_state(sd)
             h.finalize()
-            self._native, self._native_version = h, ver
-        return self._native
+            cache[ver] = h
+        self._native, self._native_version = h, ver
+        return h
 
     def _sched(self):
         sch = getattr(self, '_sched_buffers', None)

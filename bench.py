@@ -28,12 +28,19 @@ Clip batches are sharded (weak scaling, B clips per rank); the noise is a
 counter-based Philox stream keyed by (seed, global sample index, round, step),
 so a clip's result does not depend on the shard it lands on.
 
+`--dist-backend gloo` runs the same rank path over gloo (collectives staged through
+host memory; ranks share the GPUs round-robin) to rehearse N > 1 on one GPU.
+
+Other BASELINE workloads: `--config {kth,cityscapes,ucf,smmnist}` (WORKLOADS below:
+each dataset's tc / tp / rounds / sampler, its wrapper and denoiser variant, a per-GPU
+batch), one bench line each; BAIR stays the default the driver runs.
+
 Output: rank 0 prints (and flushes) a JSON line as soon as the timed region and
 the roofline launch timing are done, marked "partial": true, then the complete
 line with `cpu_baseline` once the CPU port has been timed. The last line is the
 result.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config NAME]
 """
 import argparse
 import json
@@ -57,24 +64,53 @@ F16X3_PEAK_TFLOPS = 2516.6 / 3
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak
 
 
+# BASELINE.json configs as bench workloads (tc / tp per round, rounds =
+# ceil(total_pred / tp); the sampler of the dataset's eval script). `batch` = clips per GPU:
+# the BASELINE batch split over its GPU count where it names one (KTH: 64 on 4 GPUs), else
+# what one MI355X runs in a few minutes. The BAIR line is the metric (configs[1]).
+WORKLOADS = {
+    'bair': dict(image=64, tc=2, tp=14, total_pred=28, sampling_steps=1000, timesteps=1000, batch=64, occ=False,
+                 precision=None, baseline='configs[1]: BAIR 64x64 ch3, cond=2 pred=14, DDPM 1000 steps, 1xMI355X'),
+    'kth': dict(image=64, tc=10, tp=20, total_pred=40, sampling_steps=100, timesteps=1000, batch=16, occ=False,
+                precision=None, cpu_steady=2, baseline='configs[2]: KTH 64x64 ch1, cond=10 pred=40, DDIM 100 steps, batch=64 on 4 GPUs'),
+    'cityscapes': dict(image=128, tc=2, tp=5, total_pred=28, sampling_steps=1000, timesteps=1000, batch=8, occ=True,
+                       precision=None, cpu_steady=2, baseline='configs[3]: Cityscapes 128x128 ch3, cond=2 pred=28, DDPM 1000 steps'),
+    'ucf': dict(image=256, tc=4, tp=12, total_pred=12, sampling_steps=10, timesteps=1000, batch=4, occ=True,
+                precision='bf16_attn', cpu_steady=1, cpu_steps_max=1, baseline='configs[4]: UCF-101 256x256 ch3, cond=4 pred=12, bf16 MFMA attention'),
+    'smmnist': dict(image=64, tc=10, tp=10, total_pred=10, sampling_steps=100, timesteps=100, batch=64, occ=True,
+                    precision=None, baseline='configs[0]: SMMNIST 64x64 ch1, cond=10 pred=10, DDPM 100 steps'),
+}
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=2000,
-                    help='reverse-diffusion steps to time, rounded up to whole generations (>= 1)')
+    ap.add_argument('--config', default='bair', choices=sorted(WORKLOADS),
+                    help='BASELINE workload (bair = configs[1], the metric; the others: bench lines of their own)')
+    ap.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='torch.distributed backend for N > 1 (gloo: test the rank path on one GPU)')
+    ap.add_argument('--steps', type=int, default=None,
+                    help='reverse-diffusion steps to time, rounded up to whole generations (default: one)')
     ap.add_argument('--warmup', type=int, default=5, help='untimed graph replays')
-    ap.add_argument('--batch', type=int, default=64, help='clips per GPU')
-    ap.add_argument('--sampling-steps', type=int, default=1000,
-                    help='1000 = DDPM-1000 (the metric); fewer = DDIM-S (profiling sweeps only)')
-    ap.add_argument('--total-pred', type=int, default=28)
-    ap.add_argument('--tp', type=int, default=14)
+    ap.add_argument('--batch', type=int, default=None, help='clips per GPU (default: the workload\'s)')
+    ap.add_argument('--sampling-steps', type=int, default=None,
+                    help='default: the workload\'s sampler (BAIR: DDPM-1000, the metric); fewer = DDIM-S sweeps')
+    ap.add_argument('--total-pred', type=int, default=None)
+    ap.add_argument('--tp', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-steps', type=int, default=8)
-    ap.add_argument('--precision', default=None, choices=['fp32', 'f16x3'],
+    ap.add_argument('--cpu-steps', type=int, default=3, help='timed oracle steps per CPU batch point')
+    ap.add_argument('--precision', default=None, choices=['fp32', 'f16x3', 'bf16_attn'],
                     help='conv / attention arithmetic (include/extdm.h EXTDM_PRECISION_*); default: package default')
+    ap.add_argument('--no-roofline', action='store_true', help='test-only: skip the per-kernel roofline timing')
+    ap.add_argument('--dump', default=None, help='test-only: save the gathered videos of the last generation here')
     ap.add_argument('--stub', action='store_true',
                     help='test-only: CPU/gloo stand-in workload that exercises the launcher and rank plumbing')
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    w = WORKLOADS[a.config]
+    for k in ('batch', 'sampling_steps', 'total_pred', 'tp'):
+        if getattr(a, k) is None:
+            setattr(a, k, w[k])
+    return a
 
 
 # ------------------------------------------------------------------ launcher
@@ -118,27 +154,33 @@ def synthetic_clips(B, tc, S, seed):
 
 
 class NativeWorkload:
-    """The product path: FlowDiffusion + autoregressive_sample on the HIP library."""
+    """The product path: FlowDiffusion + autoregressive_sample on the HIP library, for one of
+    the BASELINE workloads (WORKLOADS[args.config])."""
 
     def __init__(self, args, dev, world, rank):
         import importlib
         pkg = importlib.import_module(PKG)
         self.pkg, self.args, self.dev, self.world, self.rank = pkg, args, dev, world, rank
+        self.w = w = WORKLOADS[args.config]
         B = args.batch
-        wrapper, unet_arch = pkg.configs.dm_arch('bair')
-        cfg = pkg.configs.dm_config('bair', pred_frames=args.tp, sampling_timesteps=args.sampling_steps,
-                                    estimate_occlusion_map=False)
-        fd = pkg.FlowDiffusion(config=cfg, is_train=False, Unet3D_architecture=unet_arch, wrapper=wrapper).to(dev)
+        wrapper, unet_arch = pkg.configs.dm_arch(args.config)
+        cfg = pkg.configs.dm_config(args.config, pred_frames=args.tp, sampling_timesteps=args.sampling_steps,
+                                    estimate_occlusion_map=w['occ'])
+        cfg['dataset_params']['frame_shape'] = w['image']  # UCF-101 at 256 (BASELINE configs[4]; the YAML says 64)
+        fd = pkg.FlowDiffusion(config=cfg, is_train=False, Unet3D_architecture=unet_arch, wrapper=wrapper,
+                               timesteps=w['timesteps']).to(dev)
         fd.diffusion.max_batch = B
-        self.precision = args.precision or pkg._lib.DEFAULT_PRECISION
+        self.precision = args.precision or w['precision'] or pkg._lib.DEFAULT_PRECISION
         fd.unet.precision = self.precision
         self.fd = fd
         self.tc, self.tp = fd.cond_frame_num, fd.pred_frame_num
         self.rounds = -(-args.total_pred // self.tp)
         self.steps_per_generation = self.rounds * args.sampling_steps
         self.frames_per_generation = world * B * args.total_pred
-        self.clips = synthetic_clips(B, self.tc, 64, 1234 + rank).to(dev)
         self.start, _ = pkg.dist.shard(world * B, world, rank)  # weak scaling: B clips per rank
+        # the global batch from one seed, sliced per rank: a clip's input (and, with the noise
+        # keyed by global sample index, its output) does not depend on the rank count
+        self.clips = synthetic_clips(world * B, self.tc, w['image'], 1234)[self.start:self.start + B].to(dev)
         self.h = None
 
     def prime(self, warmup):
@@ -146,10 +188,11 @@ class NativeWorkload:
         capture the step graph and replay it `warmup` times, run encoder + decoder."""
         fd, B, pkg = self.fd, self.args.batch, self.pkg
         ret, x_cond, fea, ref = fd.encode(self.clips)
-        self.h = h = fd.diffusion._native(B, self.dev)
+        self.h = h = fd.diffusion._native(B, self.dev, fea.shape[-1])
         prime = torch.empty(B, 3, self.tp, x_cond.shape[3], x_cond.shape[4], device=self.dev)
-        n = max(1, warmup)
-        h.sample(pkg._lib.SAMPLER_DDPM, list(range(999, 999 - n, -1)), None, 0., x_cond, fea, prime, seed=1,
+        n = max(1, min(warmup, fd.diffusion.num_timesteps))
+        T = fd.diffusion.num_timesteps
+        h.sample(pkg._lib.SAMPLER_DDPM, list(range(T - 1, T - 1 - n, -1)), None, 0., x_cond, fea, prime, seed=1,
                  sample_base=self.start)
         fd.decode(ret, prime, ref)
         torch.cuda.synchronize()
@@ -166,41 +209,62 @@ class NativeWorkload:
         assert out.shape[0] == self.world * self.args.batch and torch.isfinite(out).all()
 
     def describe(self):
-        a, B = self.args, self.args.batch
-        sampler = 'DDPM 1000' if a.sampling_steps >= 1000 else f'DDIM {a.sampling_steps}'
+        a, B, w = self.args, self.args.batch, self.w
+        T = self.fd.diffusion.num_timesteps
+        sampler = f'DDPM {T}' if a.sampling_steps >= T else f'DDIM {a.sampling_steps} (of {T})'
+        names = {'bair': 'BAIR 64x64 ch3', 'kth': 'KTH 64x64 ch1 (as 3 ch)', 'cityscapes': 'Cityscapes 128x128 ch3',
+                 'ucf': 'UCF-101 256x256 ch3', 'smmnist': 'SMMNIST 64x64 ch1 (as 3 ch)'}
+        unet = self.fd.unet.__class__.__name__
         return {
-            'dtype': 'fp32' if self.precision == 'fp32' else
-                     'fp32 (f16x3 split-MFMA convs + attention, fp32 accumulate)',
+            'dtype': {'fp32': 'fp32', 'f16x3': 'fp32 (f16x3 split-MFMA convs + attention, fp32 accumulate)',
+                      'bf16_attn': 'fp32 convs as f16x3; attention QK^T / PV in bf16 MFMA (fp32 accumulate)'}[
+                          self.precision],
             'data': 'synthetic (U[0,1) PCG64 clips, seeded random-init weights; no dataset/checkpoint offline)',
-            'config': {'workload': f'BAIR 64x64 ch3 {self.tc}->{a.total_pred} (tp={self.tp} x {self.rounds} rounds), '
-                                   f'{sampler} steps, u12 Unet3D dim 64 mults (1,2,4,4), LFAE encoder + '
-                                   f'flow-warp decoder, no occlusion map (BAIR eval default)',
+            'config': {'workload': f'{names[a.config]} {self.tc}->{a.total_pred} (tp={self.tp} x {self.rounds} rounds), '
+                                   f'{sampler} steps, {unet} ({self.fd.wrapper} wrapper), LFAE encoder + flow-warp '
+                                   f'decoder, occlusion map {"on" if w["occ"] else "off (eval default)"}',
+                       'baseline_config': w['baseline'], 'bench_config': a.config,
                        'global_batch': self.world * B, 'batch_per_gpu': B, 'sampling_steps': a.sampling_steps,
-                       'rounds': self.rounds, 'parallelism': f'clip-shard x{self.world} (+RCCL all-gather)',
+                       'rounds': self.rounds, 'parallelism': f'clip-shard x{self.world} (+all-gather)',
                        'workspace_gb': round(self.h.workspace_bytes() / 2 ** 30, 2)}}
 
     # extdm_bench_layer ids (runtime.cpp) of the kernels reported, dominant first: the
-    # level-0 ResnetBlock 3x3 conv (64 -> 64 at 32x32, the largest share of GPU time per
-    # step, profiles/r02_*_kernel_stats.csv; block1's conv stages an fp32 input, block2's
-    # copies block1's pre-split operand, id 5), init_conv's cond_fea branch (256 -> 64,
-    # 7x7; the x-branch is the composed xpath_x3 kernel) and the level-0 1x1 res_conv
-    # (128 -> 64), which is HBM-bound: 3 FLOP-equivalents of f16x3 MFMA per 4-B element
-    # moved is far below the machine balance, so it is priced against HBM bytes.
-    LAYERS = [(1, 'mfma', 'conv_x3_kernel<3,1,64,256,1,4,4,2,SPAN,NS=2>', 'level-0 ResnetBlock block1 conv 64->64 1x3x3, fp32 input staged', 64, 64),
-              (5, 'mfma', 'conv_x3_kernel<3,1,64,256,1,4,4,2,SPAN,XOP>', 'level-0 ResnetBlock block2 conv 64->64 1x3x3, pre-split operand by LDS-DMA', 64, 64),
-              (0, 'mfma', 'conv_x3_kernel<7,1,64,512,1,8,16,1>', 'init_conv cond_fea branch 256->64 1x7x7', 256, 64),
-              (4, 'hbm', 'conv_x3_kernel<1,1,64,128,2,4,4,2>', 'level-0 res_conv 128->64 1x1x1', 128, 64)]
+    # level-0 ResnetBlock 3x3 conv (64 -> 64 at the latent size; block1's conv stages an fp32
+    # input, block2's copies block1's pre-split operand, id 5), init_conv's cond_fea branch
+    # (256 -> 64, 7x7), the level-0 1x1 res_conv (128 -> 64, HBM-bound: 3 FLOP-equivalents
+    # of f16x3 MFMA per 4-B element moved is far below the machine balance), and the
+    # attention launches: level-0 shifted-window attention (6), the temporal attention (7)
+    # and TrajWarp's cross-attention core (8). `kernel`: the launched template; the PMC
+    # traffic of profiles/pmc_layer<id>.json counts only when it names this template and
+    # was measured on this exact library build (lib_sha16).
+    LAYERS = [(1, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0>',
+               'level-0 ResnetBlock block1 conv 64->64 1x3x3, fp32 input staged'),
+              (6, 'mfma', 'attn_x3_kernel<64, 0, 32, 8>',
+               'level-0 shifted-window attention (STW, C 64, 2x4x4 windows, 8 heads x 32), fused LN/qkv/proj'),
+              (5, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true, false, 0>',
+               'level-0 ResnetBlock block2 conv 64->64 1x3x3, pre-split operand by LDS-DMA'),
+              (0, 'mfma', 'conv_x3_kernel<7, 1, 64, 512, 1, 8, 16, 1, true, 1, false, false, 0>',
+               'init_conv cond_fea branch 256->64 1x7x7'),
+              (7, 'mfma', 'attn_x3_kernel<64, 1, 32, 8>', 'init_temporal_attn (C 64, 16 frames, 8 heads x 32)'),
+              (8, 'mfma', 'cross_attn_x3p_kernel', 'TrajWarp cross-attention core (3584 queries x 512 keys, 8 heads)'),
+              (4, 'hbm', 'conv_x3_kernel<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, false, 0>',
+               'level-0 res_conv 128->64 1x1x1')]
 
-    def _traffic(self, layer):
-        """HBM bytes per launch from the committed PMC passes (scripts_gpu/pmc_layers.sh)."""
+    def _traffic(self, layer, kname):
+        """HBM bytes per launch from the committed PMC passes (scripts_gpu/pmc_layers.sh), only
+        when they were taken on this library build and name the launched template."""
         pmc = os.path.join(REPO, 'profiles', f'pmc_layer{layer}.json')
         try:
             j = json.load(open(pmc))
-            if int(j.get('batch', -1)) == self.args.batch and j.get('precision') == self.precision:
-                return j.get('hbm_bytes_per_launch')
         except (ValueError, OSError):
-            pass
-        return None
+            return None, 'no PMC file'
+        if int(j.get('batch', -1)) != self.args.batch or j.get('precision') != self.precision:
+            return None, 'PMC batch / precision differ'
+        if j.get('lib_sha16') != lib_sha16():
+            return None, 'PMC taken on another library build (stale)'
+        if kname not in j.get('kernel_name', ''):
+            return None, 'PMC kernel signature differs'
+        return j.get('hbm_bytes_per_launch'), 'profiles/' + os.path.basename(pmc)
 
     def roofline(self):
         """Per kernel, timed over 20 launches of the exact forward launch with HIP events
@@ -209,33 +273,51 @@ class NativeWorkload:
         launch (fp32 input + output elements, 4 B each, weights aside) / time against
         8 TB/s. The first entry is the dominant kernel; the others ride along."""
         B = self.args.batch
-        peak = F16X3_PEAK_TFLOPS if self.precision == 'f16x3' else FP32_MFMA_PEAK_TFLOPS
+        peak = FP32_MFMA_PEAK_TFLOPS if self.precision == 'fp32' else F16X3_PEAK_TFLOPS
         u = self.fd.unet.ucfg
         T = self.tc + self.tp
         out = []
-        for layer, bound, kname, what, cin, cout in self.LAYERS:
-            if layer == 5 and self.precision != 'f16x3':
+        for layer, bound, kname, what in self.LAYERS:
+            if layer == 5 and self.precision == 'fp32':
                 continue
-            ms_layer, flops = self.h.bench_layer(B, layer, 20)
-            traffic = self._traffic(layer)
+            try:
+                ms_layer, flops = self.h.bench_layer(B, layer, 20)
+            except RuntimeError:  # the layer does not exist in this denoiser variant / precision
+                continue
+            traffic, src = self._traffic(layer, kname)
             if bound == 'mfma':
                 achieved = flops / (ms_layer * 1e-3) / 1e12
                 e = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
                      'frac': round(achieved / peak, 4), 'flop_per_launch': flops}
             else:
+                cin, cout = 128, 64
                 nbytes = 4 * B * T * u.latent * u.latent * (cin + cout)
                 achieved = nbytes / (ms_layer * 1e-3) / 1e9
                 e = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'bytes_per_launch': nbytes}
-            e.update({'kernel': f'{kname} ({what}, {self.precision})', 'traffic': traffic,
+            e.update({'kernel': f'{kname} ({what}, {self.precision})', 'traffic': traffic, 'traffic_src': src,
                       'launch_ms': round(ms_layer, 4)})
             out.append(e)
+        if not out:
+            return None
         res = out[0]
         res['others'] = out[1:]
         return res
 
     def cpu_baseline(self):
-        return cpu_baseline(self.fd, self.rounds, self.args.sampling_steps, self.args.cpu_steps)
+        return cpu_baseline(self.fd, self.rounds, self.args.sampling_steps,
+                            min(self.args.cpu_steps, self.w.get('cpu_steps_max', self.args.cpu_steps)), self.w,
+                            steady_batch=self.w.get('cpu_steady', 4))
+
+
+def lib_sha16():
+    """First 16 hex digits of sha256 of the loaded HIP library (EXTDM_LIB or the in-tree one)."""
+    import hashlib
+    path = os.environ.get('EXTDM_LIB') or os.path.join(REPO, PKG, 'libextdm_hip.so')
+    try:
+        return hashlib.sha256(open(path, 'rb').read()).hexdigest()[:16]
+    except OSError:
+        return None
 
 
 class StubWorkload:
@@ -291,44 +373,73 @@ def cpu_model():
     return 'unknown'
 
 
-def cpu_baseline(fd, rounds, steps_per_round, n_steps):
-    """The oracle (PyTorch-CPU restatement of the reference, kind "port") timed on
-    this box's host cores at B = 1: one round's LFAE encoder, n_steps DDPM steps
-    (Unet forward + p_sample update) and one round's decode, extrapolated to the
-    same 2 -> 28 workload. Oracle use is confined to this untimed checker leg."""
+def cpu_threads():
+    """Host cores this process may run on (sched affinity) and the threads the CPU
+    baseline uses: OMP_NUM_THREADS where set (the GPU box's per-GPU CPU share), else all."""
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    env = os.environ.get('OMP_NUM_THREADS')
+    threads = min(cores, int(env)) if env and env.isdigit() and int(env) > 0 else cores
+    return cores, threads
+
+
+def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
+    """The oracle (PyTorch-CPU restatement of the reference, kind "port") timed on this
+    box's host cores at B = 1 and at a steady batch: one round's LFAE
+    encoder and decode (B = 1, scaled by B), n_steps reverse steps (Unet forward + the
+    DDPM / DDIM update) per batch point, extrapolated to the workload's rounds x steps;
+    the better batch point is `value`. Oracle use is confined to this untimed leg."""
     from oracle import extdm_oracle as O
     from oracle import lfae_oracle as LO
+    cores, threads = cpu_threads()
+    torch.set_num_threads(threads)
     ucfg = fd.unet.ucfg
     lc = fd.lcfg
     sd = {f'generator.{k}': v.detach().cpu() for k, v in fd.generator.state_dict().items()}
     sd.update({f'region_predictor.{k}': v.detach().cpu() for k, v in fd.region_predictor.state_dict().items()})
     sd.update({f'bg_predictor.{k}': v.detach().cpu() for k, v in fd.bg_predictor.state_dict().items()})
     usd = {k: v.detach().cpu() for k, v in fd.unet.state_dict().items()}
-    sch = O.schedule(1000)
+    T_sched = fd.diffusion.num_timesteps
+    sch = O.schedule(T_sched)
+    ddim = steps_per_round < T_sched
     vid = synthetic_clips(1, ucfg.tc, lc.image, 99)
     with torch.no_grad():
         t0 = time.perf_counter()
         ret, x_cond, fea, ref = LO.encode_round(sd, lc, ucfg, vid)
         t_enc = time.perf_counter() - t0
+        if fd.wrapper == 'multi1248':  # cond_fea at flow size, tc - 1 + tp frames (multi1248.py:240-245)
+            fea = torch.randn(1, fea.shape[1], ucfg.tc - 1 + ucfg.tp, ucfg.latent, ucfg.latent)
         x = torch.randn(1, 3, ucfg.tp, ucfg.latent, ucfg.latent)
-        t = torch.full((1,), 999, dtype=torch.long)
-        O.ddpm_step(sch, x, O.unet_forward(usd, ucfg.as_dict(), x, t, x_cond, fea), t, torch.randn_like(x))  # warm
-        per = []
-        for k in range(n_steps):
-            t = torch.full((1,), 998 - k, dtype=torch.long)
-            t0 = time.perf_counter()
-            x = O.ddpm_step(sch, x, O.unet_forward(usd, ucfg.as_dict(), x, t, x_cond, fea), t, torch.randn_like(x))
-            per.append(time.perf_counter() - t0)
-        t_step = float(np.median(per))
         t0 = time.perf_counter()
         LO.decode_round(sd, lc, ucfg, ret, x, ref)
         t_dec = time.perf_counter() - t0
-    total = rounds * (t_enc + steps_per_round * t_step + t_dec)
-    return {'value': round(rounds * ucfg.tp / total, 5), 'unit': 'frames/s', 'cores': torch.get_num_threads(),
-            'kind': 'port', 'cpu_model': cpu_model(),
-            'sample': f'oracle (PyTorch-CPU fp32) B=1: encoder round ({t_enc:.3f} s), {n_steps} DDPM steps '
-                      f'(median {t_step:.3f} s/step, range {min(per):.3f}-{max(per):.3f}), decode round '
-                      f'({t_dec:.3f} s); extrapolated to {rounds} rounds x {steps_per_round} steps'}
+        points = []
+        for B in ([1, steady_batch] if steady_batch > 1 else [1]):
+            xc, fb, xb = x_cond.expand(B, *x_cond.shape[1:]), fea.expand(B, *fea.shape[1:]), x.expand(B, *x.shape[1:])
+
+            def step(k, xb):
+                t = torch.full((B,), T_sched - 1 - k, dtype=torch.long)
+                eps = O.unet_forward(usd, ucfg.as_dict(), xb, t, xc, fb)
+                if ddim:
+                    return O.ddim_step(sch, xb, eps, t, t - 1, torch.randn_like(xb))
+                return O.ddpm_step(sch, xb, eps, t, torch.randn_like(xb))
+            xb = step(0, xb)  # warm
+            per = []
+            for k in range(n_steps):
+                t0 = time.perf_counter()
+                xb = step(k + 1, xb)
+                per.append(time.perf_counter() - t0)
+            t_step = float(np.median(per))
+            total = rounds * B * (t_enc + t_dec) + rounds * steps_per_round * t_step
+            points.append({'batch': B, 'frames_per_s': round(rounds * ucfg.tp * B / total, 5),
+                           's_per_step': round(t_step, 4)})
+    best = max(points, key=lambda p: p['frames_per_s'])
+    return {'value': best['frames_per_s'], 'unit': 'frames/s', 'cores': cores, 'threads': threads,
+            'kind': 'port', 'cpu_model': cpu_model(), 'batch_points': points,
+            'sample': f'oracle (PyTorch-CPU fp32) on {threads} threads of {cores} host cores: encoder round '
+                      f'({t_enc:.3f} s) and decode round ({t_dec:.3f} s) at B=1, {n_steps} '
+                      f'{"DDIM" if ddim else "DDPM"} steps per batch point (B = '
+                      f'{", ".join(str(p["batch"]) for p in points)}); extrapolated to {rounds} rounds x '
+                      f'{steps_per_round} steps; value = the better batch point (B={best["batch"]})'}
 
 
 # ------------------------------------------------------------------ rank body
@@ -343,14 +454,19 @@ def run_rank(args):
             dist.init_process_group('gloo')
         wl = StubWorkload(args, dev, world, rank)
     else:
-        torch.cuda.set_device(local)
-        dev = torch.device('cuda', local)
+        # one GPU per rank; with fewer GPUs than ranks (the gloo rehearsal on a 1-GPU box) the
+        # ranks share them round-robin (device_count does not initialise the GPU)
+        dev = torch.device('cuda', local % max(1, torch.cuda.device_count()))
+        torch.cuda.set_device(dev)
         if world > 1:
-            dist.init_process_group('nccl', device_id=dev)
+            if args.dist_backend == 'nccl':
+                dist.init_process_group('nccl', device_id=dev)
+            else:
+                dist.init_process_group('gloo')
         wl = NativeWorkload(args, dev, world, rank)
     D = importlib_dist()
     wl.prime(args.warmup)
-    gens = max(1, math.ceil(args.steps / wl.steps_per_generation))
+    gens = max(1, math.ceil((args.steps or 1) / wl.steps_per_generation))
     if world > 1:
         dist.barrier()
     wl.sync()
@@ -360,21 +476,23 @@ def run_rank(args):
     wl.sync()
     if world > 1:
         dist.barrier()
-    el = D.max_over_ranks(time.perf_counter() - t0, device=dev)
+    el = D.max_over_ranks(time.perf_counter() - t0, device=dev if args.dist_backend == 'nccl' else None)
     steps = gens * wl.steps_per_generation
     value = wl.frames_per_generation * gens / el
     result = None
     if rank == 0:
         wl.check(out)
+        if args.dump:
+            torch.save(out.detach().cpu(), args.dump)
         meta = json.load(open(os.path.join(REPO, 'BASELINE.json')))
         result = {'metric': meta['metric'], 'value': round(value, 4), 'unit': 'frames/s', 'n_gpus': world,
                   'steps': steps, 'warmup': args.warmup, 'ms_per_step': round(el / steps * 1e3, 4),
                   'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None}
         result.update(wl.describe())
         result['generations'] = gens
-        result['requested_steps'] = args.steps
+        result['requested_steps'] = args.steps if args.steps is not None else wl.steps_per_generation
         result['timed_s'] = round(el, 3)
-        result['roofline'] = wl.roofline()
+        result['roofline'] = None if args.no_roofline else wl.roofline()
         result['partial'] = True
         print(json.dumps(result), flush=True)
     if world > 1:

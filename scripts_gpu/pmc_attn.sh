@@ -6,7 +6,7 @@ TAG=${TAG:-pa}
 i=0
 for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_MFMA"; do
   rm -rf gpurun_out/${TAG}_p$i
-  timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/${TAG}_p$i -o run --output-format csv -- python scripts_gpu/attn_dbg.py 64 > gpurun_out/${TAG}_p$i.log 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/${TAG}_p$i -o run --output-format csv -- python scripts_gpu/attn_dbg.py 64 5 > gpurun_out/${TAG}_p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/${TAG}_p$i.log; exit $rc; }
   i=$((i+1))
 done

@@ -1,0 +1,17 @@
+#!/bin/bash
+# SQ counters of the fused attention kernels, full and without the unit loop (EXTDM_X3_DBG=16),
+# so that the unit loop's share is the difference. Two --pmc passes per arm.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${TAG:-pa2}
+for d in 0 16; do
+  i=0
+  for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_MFMA"; do
+    rm -rf gpurun_out/${TAG}_d${d}_p$i
+    EXTDM_X3_DBG=$d timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace -d gpurun_out/${TAG}_d${d}_p$i -o run --output-format csv -- python scripts_gpu/attn_dbg.py 64 5 > gpurun_out/${TAG}_d${d}_p$i.log 2>&1
+    rc=$?; echo "dbg $d pass $i rc=$rc"; [ $rc -ne 0 ] && { tail -5 gpurun_out/${TAG}_d${d}_p$i.log; exit $rc; }
+    i=$((i+1))
+  done
+  python scripts_gpu/pmc_table.py gpurun_out/${TAG}_d${d}_p0 gpurun_out/${TAG}_d${d}_p1 > gpurun_out/${TAG}_d${d}_table.txt
+  find gpurun_out/${TAG}_d${d}_p0 gpurun_out/${TAG}_d${d}_p1 -name "*kernel_trace.csv" -delete
+done
+grep -A17 "attn_x3_kernelILi64ELi0ELi32ELi8ELb1" gpurun_out/${TAG}_d0_table.txt gpurun_out/${TAG}_d16_table.txt

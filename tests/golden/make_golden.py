@@ -7,7 +7,7 @@ replaced by the stand-ins under tests/golden/shims/ (einops_exts, timm,
 skimage: import-only; rotary_embedding_torch: restatement of 0.8.3; cv2: the two
 OpenCV calls of calculate_ssim.py restated).
 
-Usage (build container only):  python tests/golden/make_golden.py
+Usage (build container only):  python tests/golden/make_golden.py [--variants|--lfae|--wrappers|--metrics|--e2e]
 """
 import importlib
 import json
@@ -198,6 +198,96 @@ def wrappers():
     np.savez_compressed(os.path.join(HERE, 'wrappers.npz'), **out)
 
 
+def e2e():
+    """End-to-end sampling at the other BASELINE configs' shapes (tests/golden/e2e.npz;
+    tests/golden_inputs.py E2E): KTH DDIM-100 (ada), Cityscapes 5 DDPM steps (ada_u22,
+    latent 32), UCF-101 256 sample_one_video (multi_w_ref_u22, DDIM-10) and SMMNIST 10 -> 10
+    as two DDPM-100 rounds through multi1248. Noise: torch.manual_seed(noise_seed) right
+    before the reference call; the tests replay the same CPU stream."""
+    import types
+    from math import ceil
+    from tests.golden_inputs import E2E, E2E_UCF_FULL
+    from model.BaseDM_adaptor.Diffusion import GaussianDiffusion
+    out = {}
+    # KTH 10 -> 20, ada, DDIM-100 over the 1000-step schedule
+    c = E2E['kth_ddim100']
+    cfg = c['unet']
+    net = build_ref_unet(importlib.import_module('model.BaseDM_adaptor.' + REF_MODULES['ada']).Unet3D, cfg)
+    net.load_state_dict(make_sd(cfg), strict=True)
+    x, _, cond, fea = unet_inputs(cfg, B=1, seed=c['seed'])
+    d = GaussianDiffusion(net, image_size=cfg.latent, num_frames=cfg.tc + cfg.tp, timesteps=1000,
+                          sampling_timesteps=c['S'], ddim_sampling_eta=1.0, null_cond_prob=0.0)
+    torch.manual_seed(c['noise_seed'])
+    with torch.no_grad():
+        out['kth_ddim100'] = d.sample(cond, cond_fea=fea).numpy()
+    print('kth_ddim100', out['kth_ddim100'].shape)
+    # Cityscapes latent 32, ada_u22: DDPM steps t = 999..995 (p_sample with the evident binding)
+    c = E2E['city_ddpm5']
+    cfg = c['unet']
+    net = build_ref_unet(importlib.import_module('model.BaseDM_adaptor.' + REF_MODULES['ada_u22']).Unet3D, cfg)
+    net.load_state_dict(make_sd(cfg), strict=True)
+    x, _, cond, fea = unet_inputs(cfg, B=1, seed=c['seed'])
+    d = GaussianDiffusion(net, image_size=cfg.latent, num_frames=cfg.tc + cfg.tp, timesteps=1000,
+                          sampling_timesteps=1000, null_cond_prob=0.0)
+    torch.manual_seed(c['noise_seed'])
+    img = torch.randn(x.shape)
+    with torch.no_grad():
+        for i in c['times']:
+            img = d.p_sample(cond, img, fea, torch.full((1,), i, dtype=torch.long))
+    out['city_ddpm5'] = img.numpy()
+    print('city_ddpm5', img.shape)
+    # UCF-101 256: multi_w_ref_u22.sample_one_video, DDIM-10
+    c = E2E['ucf256']
+    mod = importlib.import_module('model.BaseDM_adaptor.' + c['module'])
+    cfgd = c['config']()
+    lc = spec.LfaeConfig.from_config(cfgd)
+    fd = mod.FlowDiffusion(config=cfgd, pretrained_pth='', is_train=False, device_ids=['cpu', 'cpu', 'cpu']).eval()
+    _load_lfae(fd, make_lfae_sd(lc))
+    fd.unet.load_state_dict(make_sd(c['unet']), strict=True)
+    vid = video_inputs(B=c['B'], T=c['unet'].tc, S=c['image'], seed=c['seed'])
+    torch.manual_seed(c['noise_seed'])
+    with torch.no_grad():
+        ret = fd.sample_one_video(cond_scale=1.0, real_vid=vid.clone())
+    for k, v in ret.items():
+        v = v.detach()
+        if k in E2E_UCF_FULL:
+            out[f'ucf256_{k}'] = v.numpy()
+        elif k == 'sample_out_vid':
+            out[f'ucf256_{k}_sub'] = v[..., ::2, ::2].numpy()
+        out[f'ucf256_{k}_sum'] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+    print('ucf256', {k: tuple(v.shape) for k, v in ret.items()})
+    # SMMNIST 10 -> 10: two DDPM-100 rounds through multi1248. Its p_sample_loop raises as
+    # written (Diffusion.py:186 binds t to cond_fea): the evident binding, the reference's own
+    # p_sample, the loop's RNG order
+    c = E2E['smmnist_2r']
+    mod = importlib.import_module('model.BaseDM_adaptor.' + c['module'])
+    cfgd = c['config']()
+    lc = spec.LfaeConfig.from_config(cfgd)
+    fd = mod.FlowDiffusion(config=cfgd, pretrained_pth='', is_train=False, timesteps=c['timesteps']).eval()
+    _load_lfae(fd, make_lfae_sd(lc))
+    fd.unet.load_state_dict(make_sd(c['unet']), strict=True)
+
+    def loop(self, x_cond, shape, cond_fea, cond=None, cond_scale=1.):
+        img = torch.randn(shape)
+        for i in reversed(range(self.num_timesteps)):
+            img = self.p_sample(x_cond, img, cond_fea, torch.full((shape[0],), i, dtype=torch.long), cond=cond,
+                                cond_scale=cond_scale)
+        return img
+    fd.diffusion.p_sample_loop = types.MethodType(loop, fd.diffusion)
+    real = video_inputs(B=c['B'], T=c['unet'].tc, seed=c['seed'])
+    tc, tp = c['unet'].tc, c['unet'].tp
+    torch.manual_seed(c['noise_seed'])
+    preds, cur = [], real[:, :, :tc]
+    with torch.no_grad():
+        for _ in range(ceil(c['total'] / tp)):
+            pv = fd.sample_one_video(cond_scale=1.0, real_vid=cur)['sample_out_vid'].clone()
+            preds.append(pv[:, :, -tp:])
+            cur = pv[:, :, -tc:]
+    out['smmnist_2r'] = torch.cat([real[:, :, :tc], torch.cat(preds, dim=2)[:, :, :c['total']]], dim=2).numpy()
+    print('smmnist_2r', out['smmnist_2r'].shape)
+    np.savez_compressed(os.path.join(HERE, 'e2e.npz'), **out)
+
+
 def build_ref_unet(Unet3D, cfg):
     return Unet3D(dim=cfg.dim, channels=cfg.channels, out_grid_dim=2, out_conf_dim=1, dim_mults=cfg.dim_mults,
                   use_bert_text_cond=False, learn_null_cond=False, use_final_activation=False, use_deconv=True,
@@ -354,6 +444,11 @@ if __name__ == '__main__':
         import_reference()
         metrics()
         sys.exit(0)
+    if '--e2e' in sys.argv:
+        torch.set_num_threads(8)
+        import_reference()
+        e2e()
+        sys.exit(0)
     if '--variants' in sys.argv or '--lfae' in sys.argv or '--wrappers' in sys.argv:
         torch.set_num_threads(8)
         import_reference()
@@ -371,3 +466,4 @@ if __name__ == '__main__':
         lfae()
         wrappers()
         metrics()
+        e2e()

@@ -65,6 +65,36 @@ WRAP_CASES = {
 AR_CASE = {'unet': FD_UNET, 'occ': False, 'B': 1, 'n': 2, 'total': 7, 'seed': 14, 'noise_seed': 45}
 
 
+# End-to-end sampling at the other BASELINE configs' shapes (tests/golden/e2e.npz, make_golden.py
+# e2e(); VERDICT r2 'Next round' item 5):
+#   kth_ddim100  ada denoiser, KTH 10 -> 20, DDIM-100 over the 1000-step schedule (Diffusion.py:209-258)
+#   city_ddpm5   full-size ada_u22 at Cityscapes' latent 32 (cond_fea 32x32), 5 DDPM steps t = 999..995
+#   ucf256       VideoFlowDiffusion_multi_w_ref_u22.sample_one_video at UCF-101 256 px (latent 128, 64
+#                regions), DDIM-10, B = 1
+#   smmnist_2r   VideoFlowDiffusion_multi1248, SMMNIST 10 -> 10 as two DDPM-100 rounds (valid.py:141-186)
+E2E = {
+    'kth_ddim100': {'unet': CONFIGS['ada_kth'], 'seed': 51, 'noise_seed': 52, 'S': 100},
+    'city_ddpm5': {'unet': _for(_spec.ARCH_ADA_U22, tc=2, tp=5, latent=32, fea_size=32), 'seed': 53,
+                   'noise_seed': 54, 'times': list(range(999, 994, -1))},
+    'ucf256': {'module': 'VideoFlowDiffusion_multi_w_ref_u22', 'wrapper': 'multi_w_ref_u22', 'image': 256,
+               'config': lambda: _ucf256_config(), 'unet': CONFIGS['u22_ucf'], 'B': 1, 'seed': 55,
+               'noise_seed': 56},
+    'smmnist_2r': {'module': 'VideoFlowDiffusion_multi1248', 'wrapper': 'multi1248',
+                   'config': lambda: _configs.dm_config('smmnist', sampling_timesteps=100),
+                   'unet': _for(_spec.ARCH_WO_REF, tc=10, tp=5, latent=32), 'B': 1, 'total': 10, 'timesteps': 100,
+                   'seed': 57, 'noise_seed': 58},
+}
+# the UCF-256 sample_one_video keys stored whole; sample_out_vid at every second pixel, every
+# key's fp64 (sum, abs-sum) of the full tensor — to keep the fixture small
+E2E_UCF_FULL = ('real_vid_grid', 'real_vid_conf', 'sample_vid_grid', 'sample_vid_conf')
+
+
+def _ucf256_config():
+    c = _configs.dm_config('ucf', pred_frames=12, sampling_timesteps=10)
+    c['dataset_params']['frame_shape'] = 256  # BASELINE configs[4] (ucf.yaml says 64)
+    return c
+
+
 def ddpm100_case():
     """DDPM on the timesteps=100 schedule with the wo_ref denoiser (SMMNIST BASELINE config)."""
     cfg = CONFIGS['woref_small']

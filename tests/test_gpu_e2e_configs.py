@@ -1,0 +1,139 @@
+"""GPU: end-to-end sampling at the other BASELINE configs' shapes against outputs of the
+reference itself (tests/golden/e2e.npz, tests/golden/make_golden.py e2e(); VERDICT r2
+'Next round' item 5):
+
+  * KTH 10 -> 20, ada denoiser, the DDIM-100 pair list over the 1000-step schedule
+    (Diffusion.py:209-258, the alphas_cumprod_prev quirk included);
+  * Cityscapes, full-size ada_u22 at latent 32 (cond_fea 32x32), five DDPM steps
+    t = 999..995 on the 1000-step schedule;
+  * VideoFlowDiffusion_multi_w_ref_u22.sample_one_video at UCF-101 256 px (flow / latent
+    128, 64 regions), DDIM-10, B = 1, in F16X3 and BF16_ATTN;
+  * SMMNIST 10 -> 10 as two DDPM-100 rounds through VideoFlowDiffusion_multi1248 and the
+    eval driver's autoregressive loop (valid.py:141-186).
+
+The reference's CPU noise stream is replayed and injected. Tolerances (max-abs): a chain
+of reverse steps 5e-4 (DDPM-5) / 2e-3 (DDIM-100: 100 thresholded steps); a sample_one_video
+round 1e-3 as the other wrapper tests; two chained rounds 2e-3 (tests/test_gpu_wrappers.py).
+BF16_ATTN is not fp32-faithful: its UCF round is held to 5e-2 on the flow grid / occlusion
+map and the decoded frames (values in [-1, 1] / [0, 1]; the eps-level contract is
+tests/test_gpu_bf16_attn.py's 5e-3 x max|eps|)."""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_inputs import E2E, E2E_UCF_FULL, PKG, ddim_noise, make_lfae_sd, make_sd, unet_inputs, video_inputs
+from tests.test_oracle_golden import load
+
+pytestmark = pytest.mark.gpu
+pkg = importlib.import_module(PKG)
+spec = importlib.import_module(PKG + '.spec')
+DEV = torch.device('cuda:0')
+
+
+def _handle(cfg, timesteps, B, precision=None):
+    h = pkg._lib.Handle(cfg, timesteps, B, 0, precision=precision)
+    sd = make_sd(cfg)
+    sd.update(pkg.schedule_buffers(timesteps))
+    h.load_state(sd)
+    h.finalize()
+    return h
+
+
+def test_kth_ddim100_chain_vs_reference():
+    c = E2E['kth_ddim100']
+    cfg = c['unet']
+    x, _, cond, fea = unet_inputs(cfg, B=1, seed=c['seed'])
+    h = _handle(cfg, 1000, 1)
+    pairs = pkg.ddim_time_pairs(1000, c['S'])
+    assert len(pairs) == c['S']
+    torch.manual_seed(c['noise_seed'])
+    xT, noise = ddim_noise(x.shape, S=c['S'])
+    out = torch.empty(x.shape, device=DEV)
+    h.sample(pkg._lib.SAMPLER_DDIM, [p[0] for p in pairs], [p[1] for p in pairs], 1.0, cond.to(DEV), fea.to(DEV), out,
+             x_T=xT.to(DEV), noise=noise.to(DEV).contiguous(), use_graph=True)
+    torch.cuda.synchronize()
+    err = np.abs(out.cpu().numpy() - load('e2e.npz')['kth_ddim100']).max()
+    print(f'kth ddim100 max|err| {err:.2e}')
+    assert err <= 2e-3, err
+
+
+def test_cityscapes_ddpm5_full_size_vs_reference():
+    c = E2E['city_ddpm5']
+    cfg = c['unet']
+    x, _, cond, fea = unet_inputs(cfg, B=1, seed=c['seed'])
+    h = _handle(cfg, 1000, 1)
+    torch.manual_seed(c['noise_seed'])
+    xT = torch.randn(x.shape)
+    noise = torch.stack([torch.randn(x.shape) for _ in c['times']])  # p_sample draws at every step
+    out = torch.empty(x.shape, device=DEV)
+    h.sample(pkg._lib.SAMPLER_DDPM, c['times'], None, 0., cond.to(DEV), fea.to(DEV), out, x_T=xT.to(DEV),
+             noise=noise.to(DEV).contiguous(), use_graph=True)
+    torch.cuda.synchronize()
+    err = np.abs(out.cpu().numpy() - load('e2e.npz')['city_ddpm5']).max()
+    print(f'cityscapes ddpm5 max|err| {err:.2e}')
+    assert err <= 5e-4, err
+
+
+def _wrapper(case, precision=None):
+    cfgd = case['config']()
+    lc = spec.LfaeConfig.from_config(cfgd)
+    fd = pkg.FlowDiffusion(config=cfgd, is_train=False, wrapper=case['wrapper'], dim_mults=case['unet'].dim_mults,
+                           Unet3D_architecture=case['unet'].arch, timesteps=case.get('timesteps', 1000)).to(DEV)
+    sds = make_lfae_sd(lc)
+    fd.generator.load_state_dict(sds['generator'])
+    fd.region_predictor.load_state_dict(sds['region_predictor'])
+    fd.bg_predictor.load_state_dict(sds['bg_predictor'])
+    fd.unet.load_state_dict(make_sd(case['unet']))
+    if precision:
+        fd.unet.precision = precision
+    return fd, lc
+
+
+@pytest.mark.parametrize('precision,tol', [('f16x3', 1e-3), ('bf16_attn', 5e-2)])
+def test_ucf256_sample_one_video_vs_reference(precision, tol):
+    c = E2E['ucf256']
+    u = c['unet']
+    fd, lc = _wrapper(c, precision)
+    assert lc.image == 256 and fd.unet.ucfg.latent == 128
+    vid = video_inputs(B=c['B'], T=u.tc, S=c['image'], seed=c['seed'])
+    torch.manual_seed(c['noise_seed'])
+    xT, noise = ddim_noise((c['B'], 3, u.tp, u.latent, u.latent))
+    ret = fd.sample_one_video(1.0, vid.to(DEV), x_T=xT.to(DEV), noise=noise.to(DEV).contiguous())
+    g = load('e2e.npz')
+    errs = {}
+    for k in E2E_UCF_FULL:
+        errs[k] = float(np.abs(ret[k].cpu().numpy() - g[f'ucf256_{k}']).max())
+    errs['sample_out_vid'] = float(np.abs(ret['sample_out_vid'][..., ::2, ::2].cpu().numpy() -
+                                          g['ucf256_sample_out_vid_sub']).max())
+    for k, v in ret.items():  # every key's whole-tensor sums
+        ref = g[f'ucf256_{k}_sum']
+        s = v.double()
+        assert abs(float(s.sum()) - ref[0]) <= max(4 * tol * v.numel() ** 0.5, 1e-4 * ref[1]), k
+    print(precision, {k: f'{v:.2e}' for k, v in errs.items()})
+    # the real_* keys come from the LFAE encoder alone (fp32 in every precision mode)
+    assert max(errs['real_vid_grid'], errs['real_vid_conf']) <= 1e-3, errs
+    assert max(errs.values()) <= tol, errs
+
+
+def test_smmnist_two_ddpm100_rounds_vs_reference():
+    c = E2E['smmnist_2r']
+    u = c['unet']
+    fd, lc = _wrapper(c)
+    assert fd.diffusion.num_timesteps == 100 and not fd.diffusion.is_ddim_sampling
+    real = video_inputs(B=c['B'], T=u.tc, seed=c['seed'])
+    rounds = -(-c['total'] // u.tp)
+    torch.manual_seed(c['noise_seed'])
+    shape = (c['B'], 3, u.tp, u.latent, u.latent)
+    rn = []
+    for _ in range(rounds):
+        xT = torch.randn(shape)
+        noise = torch.stack([torch.randn(shape) for _ in range(100)])  # one draw per step, t = 0 included
+        rn.append((xT.to(DEV), noise.to(DEV).contiguous()))
+    out = pkg.autoregressive_sample(fd, real.to(DEV), c['total'], num_sample_video=1, round_noise=rn)
+    g = load('e2e.npz')['smmnist_2r']
+    assert out.shape == g.shape
+    err = np.abs(out.cpu().numpy() - g).max()
+    print(f'smmnist 2 x DDPM-100 max|err| {err:.2e}')
+    assert err <= 2e-3, err

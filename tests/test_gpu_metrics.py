@@ -1,5 +1,10 @@
 """metrics.hip (extdm_frame_metrics) against the reference's metric code
-(tests/golden/metrics.npz) and the numpy oracle."""
+(tests/golden/metrics.npz) and the numpy oracle.
+
+The SSIM goldens come from the reference's ssim() running on tests/golden/shims/cv2, a
+scipy restatement of cv2.getGaussianKernel / cv2.filter2D (OpenCV is absent here): the
+1e-12 SSIM match pins the device kernel to the reference's formula and crop through that
+shim's arithmetic — parity with OpenCV's own filter arithmetic is unpinned."""
 import importlib
 import os
 
@@ -77,3 +82,18 @@ def test_eval_metrics_summary():
     idx = M.select_best(ofeat, rfeat, 3)
     best = rfeat.reshape(3, 3, -1)[np.arange(3), idx]
     assert out['fvd_best'] == pytest.approx(M.frechet_distance(ofeat, best), rel=1e-12)
+    # valid.py:207-213: one frechet_distance per trajectory, then metric_stuff
+    fl = np.array([M.frechet_distance(ofeat, rfeat.reshape(3, 3, -1)[:, t]) for t in range(3)])
+    assert out['fvd_traj_mean'] == pytest.approx(fl.mean(), rel=1e-12)
+    assert out['fvd_traj_std'] == pytest.approx(fl.std(), rel=1e-12)
+
+
+def test_single_images_2d_and_3d():
+    """img_psnr / calculate_ssim_function take [c, h, w] and, like the reference
+    (calculate_ssim.py:31-32), a 2-D [h, w] image."""
+    a, b = metric_videos('gray')
+    i1, i2 = a[0, 0, 0], b[0, 0, 0]  # [h, w]
+    p, s = mo.frame_metrics(a[:1, :1].numpy(), b[:1, :1].numpy())
+    assert M.img_psnr(i1.cuda(), i2.cuda()) == pytest.approx(float(p[0, 0]), abs=1e-9)
+    assert M.calculate_ssim_function(i1.cuda(), i2.cuda()) == pytest.approx(float(s[0, 0]), abs=1e-12)
+    assert M.calculate_ssim_function(i1[None].cuda(), i2[None].cuda()) == pytest.approx(float(s[0, 0]), abs=1e-12)

@@ -135,6 +135,8 @@ def test_f16x3_range_guard_trips():
     h = handle('bair', 'f16x3', max_batch=1)
     h.range_flag(reset=True)
     gpu_eps(h, x, t, cond, fea * 1e5)
-    assert h.range_flag(reset=True) == 1
+    # bit 0: a conv split overflowed; the attention kernels' check (bit 1) may trip too on the
+    # non-finite activations downstream
+    assert h.range_flag(reset=True) & 1
     gpu_eps(h, x, t, cond, fea)
     assert h.range_flag() == 0
