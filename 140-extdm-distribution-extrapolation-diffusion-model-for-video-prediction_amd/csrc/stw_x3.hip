@@ -379,6 +379,19 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     rcq[r >> 1] = FOLD ? c * sq : c; rsq[r >> 1] = FOLD ? sn * sq : sn;
     rck[r >> 1] = FOLD ? c * sk : c; rsk[r >> 1] = FOLD ? sn * sk : sn;
   }
+  // tile path: the factors (the same in every wave: token = lane) go to LDS as [8 float4][64
+  // lanes] and are re-read per unit (8 conflict-free ds_read_b128) instead of holding 32
+  // VGPRs through the unit loop
+  float4* const ropeL = reinterpret_cast<float4*>(tileT + C * 256 + 128);
+  if (TILE && wave == 0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      ropeL[(0 + j) * 64 + lane] = make_float4(rcq[4 * j], rcq[4 * j + 1], rcq[4 * j + 2], rcq[4 * j + 3]);
+      ropeL[(2 + j) * 64 + lane] = make_float4(rsq[4 * j], rsq[4 * j + 1], rsq[4 * j + 2], rsq[4 * j + 3]);
+      ropeL[(4 + j) * 64 + lane] = make_float4(rck[4 * j], rck[4 * j + 1], rck[4 * j + 2], rck[4 * j + 3]);
+      ropeL[(6 + j) * 64 + lane] = make_float4(rsk[4 * j], rsk[4 * j + 1], rsk[4 * j + 2], rsk[4 * j + 3]);
+    }
+  }
 
   // ---- 2. per unit of 32 qkv rows ----
   // Q^T, K^T (rows = dims, lane = token) from the unit slice W
@@ -403,6 +416,33 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       v = mma3(xh[s], xl[s], *reinterpret_cast<const h8*>(fv), *reinterpret_cast<const h8*>(fv + 512), v);
     }
   };
+  // Q^T, K^T first, the next k-step's four fragments read from LDS while this step's six
+  // MFMAs run (sched_barrier pins the order: left alone, hipcc issued each fragment pair
+  // right before its MFMAs and waited for it, exposing the LDS latency 8x per unit)
+  auto qkv_mfma = [&](const _Float16* W, f32x16& q, f32x16& k, f32x16& v) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { q[r] = 0.f; k[r] = 0.f; }
+    h8 fr[2][4];
+    auto ld = [&](int s, h8* f) __attribute__((always_inline)) {
+      const _Float16* fq = W + UL::Q + s * UL::FRAG + lane * 8;
+      const _Float16* fk = W + UL::K + s * UL::FRAG + lane * 8;
+      f[0] = *reinterpret_cast<const h8*>(fq); f[1] = *reinterpret_cast<const h8*>(fq + 512);
+      f[2] = *reinterpret_cast<const h8*>(fk); f[3] = *reinterpret_cast<const h8*>(fk + 512);
+    };
+    ld(0, fr[0]);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (s + 1 < KS) ld(s + 1, fr[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      const h8* f = fr[s & 1];
+      q = mma3(f[0], f[1], xh[s], xl[s], q);
+      k = mma3(f[2], f[3], xh[s], xl[s], k);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // V's MFMAs left to the scheduler, which can place the RoPE / split VALU of q, k (which
+    // follows in program order and does not depend on V) between them
+    v_mfma(W, v);
+  };
   // the bias / mask rows of unit u's heads (straight into the score accumulators)
   auto load_bias = [&](int u, f32x16* bia) __attribute__((always_inline)) {
 #pragma unroll
@@ -417,6 +457,17 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   // scale + RoPE of q, k; the unit's heads: S^T = bias + K Q^T (rows = keys j, lane =
   // query i), softmax, O^T = V^T P^T
   auto attend = [&](f32x16& q, f32x16& k, const f32x16& v, const f32x16* bia) __attribute__((always_inline)) {
+    if (TILE) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float4 a = ropeL[(0 + j) * 64 + lane], bq = ropeL[(2 + j) * 64 + lane];
+        const float4 ck = ropeL[(4 + j) * 64 + lane], dk = ropeL[(6 + j) * 64 + lane];
+        rcq[4 * j] = a.x; rcq[4 * j + 1] = a.y; rcq[4 * j + 2] = a.z; rcq[4 * j + 3] = a.w;
+        rsq[4 * j] = bq.x; rsq[4 * j + 1] = bq.y; rsq[4 * j + 2] = bq.z; rsq[4 * j + 3] = bq.w;
+        rck[4 * j] = ck.x; rck[4 * j + 1] = ck.y; rck[4 * j + 2] = ck.z; rck[4 * j + 3] = ck.w;
+        rsk[4 * j] = dk.x; rsk[4 * j + 1] = dk.y; rsk[4 * j + 2] = dk.z; rsk[4 * j + 3] = dk.w;
+      }
+    }
     // scale, RoPE on (d, d+1) = registers (r, r+1); d = dof(r, h) within the head
 #pragma unroll
     for (int r = 0; r < 16; r += 2) {
@@ -522,8 +573,12 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       if (u + 1 < UNITS) load_unit(u + 1, wsm + ((u + 1) & 1) * UL::HALVES);
       if (!active) continue;
       f32x16 q, k, v;
-      qk_mfma(W, q, k);
-      v_mfma(W, v);
+      if (TILE) {
+        qkv_mfma(W, q, k, v);
+      } else {
+        qk_mfma(W, q, k);
+        v_mfma(W, v);
+      }
       const f32x16 o = attend(q, k, v, bia);
       proj(W, o);
     }
@@ -650,7 +705,7 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
   const size_t ring = (size_t)2 * UnitLayout<C>::HALVES * sizeof(_Float16);
   const bool tile = MODE == 0 && C == 64 && NW == 8 && attn_x3_tile_ok(x, out, g, groups);
   size_t lds = (MODE == 1 && C == 64 && NW == 8) ? std::max(ring, (size_t)C * 328 * sizeof(float)) : ring;
-  if (tile) lds = ring + ((size_t)C * 8 * 32 + 2 * 64) * sizeof(float);
+  if (tile) lds = ring + ((size_t)C * 8 * 32 + 2 * 64 + 8 * 64 * 4) * sizeof(float);
   // per device, once: the dynamic-LDS limit
   static std::once_flag once[64];
   int dev = 0;
