@@ -416,11 +416,14 @@ def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
         for B in ([1, steady_batch] if steady_batch > 1 else [1]):
             xc, fb, xb = x_cond.expand(B, *x_cond.shape[1:]), fea.expand(B, *fea.shape[1:]), x.expand(B, *x.shape[1:])
 
+            pairs = O.ddim_pairs(T_sched, steps_per_round) if ddim else None
+
             def step(k, xb):
-                t = torch.full((B,), T_sched - 1 - k, dtype=torch.long)
+                ti = pairs[k][0] if ddim else T_sched - 1 - k
+                t = torch.full((B,), ti, dtype=torch.long)
                 eps = O.unet_forward(usd, ucfg.as_dict(), xb, t, xc, fb)
                 if ddim:
-                    return O.ddim_step(sch, xb, eps, t, t - 1, torch.randn_like(xb))
+                    return O.ddim_step(sch, xb, eps, pairs[k][0], pairs[k][1], torch.randn_like(xb))
                 return O.ddpm_step(sch, xb, eps, t, torch.randn_like(xb))
             xb = step(0, xb)  # warm
             per = []

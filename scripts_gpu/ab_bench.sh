@@ -12,7 +12,7 @@ for i in $(seq $R); do
   for arm in cur $LIBS; do
     if [ $arm = cur ]; then unset EXTDM_LIB; else export EXTDM_LIB=_variants/$arm/libextdm_hip.so; fi
     if [ -n "$ATTN" ]; then timeout -k 10 120 python scripts_gpu/attn_dbg.py $B > gpurun_out/ab_attn_$arm.log 2>&1 || exit $?; echo "$arm $(cat gpurun_out/ab_attn_$arm.log | grep dbg)"; fi
-    timeout -k 10 300 python bench.py --sampling-steps $S --steps $S --warmup 5 --batch $B --no-cpu-baseline > gpurun_out/ab_$arm.json 2> gpurun_out/ab_$arm.err || { tail -5 gpurun_out/ab_$arm.err; exit 1; }
-    python -c "import json,sys; d=json.loads(open('gpurun_out/ab_$arm.json').read().strip().splitlines()[-1]); print('$arm', '$i', 'ms/step', d['ms_per_step'], 'layers', d['roofline']['launch_ms'], [o['launch_ms'] for o in d['roofline']['others']])"
+    timeout -k 10 300 python bench.py --sampling-steps $S --steps $S --warmup 5 --batch $B --no-cpu-baseline --no-roofline > gpurun_out/ab_$arm.json 2> gpurun_out/ab_$arm.err || { tail -5 gpurun_out/ab_$arm.err; exit 1; }
+    python -c "import json,sys; d=json.loads(open('gpurun_out/ab_$arm.json').read().strip().splitlines()[-1]); print('$arm', '$i', 'ms/step', d['ms_per_step'])"
   done
 done
