@@ -29,7 +29,10 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=o
 # them in VGPRs (the convs' accumulators only meet VALU in the epilogue and keep AGPRs).
 VGPR_MFMA = ['-mllvm', '-amdgpu-mfma-vgpr-form=1']
 PER_FILE = {'stw_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA, 'cross_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA,
-            'attn_core.hip': VGPR_MFMA}
+            'attn_core.hip': VGPR_MFMA,
+            # the scaled-lo gather split as v_mul + v_fma_mixlo per value (SLP packed it into
+            # v_pk_mul / v_pk_fma_f32 with the hi converted back: ~9 VALU per pair)
+            'xpath_x3.hip': ['-fno-slp-vectorize']}
 OPT = {}
 
 

@@ -45,32 +45,44 @@ template <> struct Frag<false> {
 };
 template <> struct Frag<true> {
   h8 hi, lo;
+  // hi = fp16(x), lo = fp16((x - hi) * 2^11): the scaled lo stays normal down to |x| ~ 2^-14
+  // (q / k / v here are 1x1-conv outputs of any scale, probabilities in [0, 1]); the cross
+  // products accumulate apart from hi * hi (mma below, as cross_x3.hip).
   // CHECK: OR |x| >= 65504 (fp16 overflow of hi) into bad; probabilities skip it.
-  // Compiler-visible split2c, not the split2 asm of kernels.h: the fragments feed MFMAs,
-  // and only compiler-visible VALU gets its MFMA hazard waits.
+  // Compiler-visible VALU, not the split2 asm of kernels.h: the fragments feed MFMAs, and
+  // only compiler-visible VALU gets its MFMA hazard waits.
   template <bool CHECK = true>
   __device__ void set(const float* x, int& bad) {
     float m = 0.f;
+    const float one = split_src(1.0f);
 #pragma unroll
-    for (int e = 0; e < 8; e += 2) {  // split2c (kernels.h): 4 VALU per pair
+    for (int e = 0; e < 8; e += 2) {
       const float w0 = split_src(x[e]), w1 = split_src(x[e + 1]);
       if (CHECK) m = fmaxf(fmaxf(m, fabsf(w0)), fabsf(w1));
-      f16x2_t ph, pl;
-      split2c(w0, w1, ph, pl);
+      const f16x2_t ph = __builtin_convertvector((f32x2_t){w0, w1}, f16x2_t);
       hi[e] = ph.x; hi[e + 1] = ph.y;
-      lo[e] = pl.x; lo[e + 1] = pl.y;
+      lo[e] = (_Float16)(__builtin_fmaf(-(float)ph.x, one, w0) * X3_LO_UP);
+      lo[e + 1] = (_Float16)(__builtin_fmaf(-(float)ph.y, one, w1) * X3_LO_UP);
     }
     if (CHECK) bad |= m >= 65504.f;
   }
 };
-// c += A * B (rows of A x columns of B over 16 k)
-__device__ __forceinline__ f32x16 mma(const Frag<false>& a, const Frag<false>& b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v, b.v, c, 0, 0, 0);
+// c += A * B (rows of A x columns of B over 16 k); f16x3: c += A_hi B_hi, x += the two cross
+// products with a scaled lo (x carries 2^11; fin combines c + 2^-11 x)
+__device__ __forceinline__ void mma(const Frag<false>& a, const Frag<false>& b, f32x16& c, f32x16&) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.v, b.v, c, 0, 0, 0);
 }
-__device__ __forceinline__ f32x16 mma(const Frag<true>& a, const Frag<true>& b, f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.lo, b.hi, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.lo, c, 0, 0, 0);
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.hi, c, 0, 0, 0);
+__device__ __forceinline__ void mma(const Frag<true>& a, const Frag<true>& b, f32x16& c, f32x16& x) {
+  x = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.lo, b.hi, x, 0, 0, 0);
+  x = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.lo, x, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.hi, c, 0, 0, 0);
+}
+template <bool X3>
+__device__ __forceinline__ void fin(f32x16& c, const f32x16& x) {
+  if (X3) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) c[r] = __builtin_fmaf(x[r], 1.f / X3_LO_UP, c[r]);
+  }
 }
 
 __device__ __forceinline__ int dof(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
@@ -209,10 +221,12 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
       f32x16 sc[NT];
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt) {
+        f32x16 sx;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sc[kt][r] = 0.f;
+        for (int r = 0; r < 16; ++r) { sc[kt][r] = 0.f; sx[r] = 0.f; }
 #pragma unroll
-        for (int s = 0; s < 2; ++s) sc[kt] = mma(kf[kt][s], qf[qt][s], sc[kt]);
+        for (int s = 0; s < 2; ++s) mma(kf[kt][s], qf[qt][s], sc[kt], sx);
+        fin<X3>(sc[kt], sx);
       }
       const TokB& me = tq[qt];
       const float* bd = bias_dense + ((long)hd * bstride + me.rpos) * bstride;
@@ -243,9 +257,9 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
       sum += __shfl_xor(sum, 32);
       const float inv = 1.f / sum;
       // ---- O^T = V^T P^T over 2 NT k-steps of 16 keys ----
-      f32x16 out;
+      f32x16 out, ox;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) out[r] = 0.f;
+      for (int r = 0; r < 16; ++r) { out[r] = 0.f; ox[r] = 0.f; }
 #pragma unroll
       for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
@@ -259,8 +273,9 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
           Frag<X3> pf, vf;
           pf.template set<false>(pv, bad);
           vf.set(vv, bad);
-          out = mma(vf, pf, out);
+          mma(vf, pf, out, ox);
         }
+      fin<X3>(out, ox);
       // out[r] = O[query qt*32 + c][dim dof(r, h)]
       if (me.valid) {
         float* ob = o + (long)b * osb + me.pos;

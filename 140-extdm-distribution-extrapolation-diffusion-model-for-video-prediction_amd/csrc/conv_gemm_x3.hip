@@ -185,7 +185,7 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
       float am = 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        split2(breg[g2][2 * e], breg[g2][2 * e + 1], hw[e], lw[e]);
+        split2s(breg[g2][2 * e], breg[g2][2 * e + 1], hw[e], lw[e]);
         amax2(am, breg[g2][2 * e], breg[g2][2 * e + 1]);
       }
       bad |= am >= 65504.f;
@@ -219,12 +219,13 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
     load_tile(kt + 1 < a.nkt ? kt + 1 : kt);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      h8 ah[TM], al[TM], bh[TN], bl[TN];
+      h8 ah[TM], al[TM], ad[TM], bh[TN], bl[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const _Float16* p = As + ((s * M32 + wm * TM + i) * 2) * 512 + lane * 8;
         ah[i] = *reinterpret_cast<const h8*>(p);
         al[i] = *reinterpret_cast<const h8*>(p + 512);
+        ad[i] = lo_dn(ah[i]);  // pairs with the scaled B lo (split2s, kernels.h)
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[i], bl[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
     }

@@ -38,6 +38,33 @@ __device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned&
       : "=&v"(hi), "=v"(lo), "=&v"(da), "=&v"(db)
       : "v"(a), "v"(b));
 }
+// Scaled-lo split of a conv activation operand: hi = fp16_rn(v), lo = fp16_rn((v - hi) * 2^11).
+// An unscaled lo is fp16-subnormal once |v| < 2^-3 (|v - hi| < 2^-14), so a tensor of small
+// activations lost bits in every lo (the f16x3 error grew as 2^-25 / |v| instead of staying
+// ~2^-23 relative: tests/test_gpu_precision.py activation-scale cases). Scaled, lo stays normal
+// down to |v| ~ 2^-14 (hi's own normal range). The conv MFMA pairs it with the weight hi
+// scaled by 2^-11 (lo_dn below), so the three products still share one accumulator:
+//   a_lo * b_hi + a_hi * (b_lo' * 2^-11) = a_lo * b_hi + (a_hi * 2^-11) * b_lo'.
+// The weight side's product is exact while a_hi * 2^-11 is normal (|a_hi| >= 2^-3 in the
+// row-scaled units, whose row maximum is 2^14..2^15); the few smaller weights lose bits only
+// in a term 2^-17 below the row's largest. Same LDS-only rule as split2.
+__device__ __forceinline__ void split2s(float a, float b, unsigned& hi, unsigned& lo) {
+  float da, db;
+  asm("v_cvt_pk_f16_f32 %0, %4, %5\n\t"
+      "v_fma_mix_f32 %2, -%0, 1.0, %4 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mix_f32 %3, -%0, 1.0, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
+      "v_ldexp_f32 %2, %2, 11\n\t"
+      "v_ldexp_f32 %3, %3, 11\n\t"
+      "v_cvt_pk_f16_f32 %1, %2, %3"
+      : "=&v"(hi), "=v"(lo), "=&v"(da), "=&v"(db)
+      : "v"(a), "v"(b));
+}
+constexpr float X3_LO_UP = 2048.f;
+// the weight-side factor of the scaled-lo product (exact power of two, 4 v_pk_mul_f16 per h8)
+template <typename H8>
+__device__ __forceinline__ H8 lo_dn(const H8& w) {
+  return w * (_Float16)(1.f / 2048.f);
+}
 // The same split in compiler-visible code (v_cvt_pk_f16_f32 of the pair, two v_fma_mix_f32
 // reading hi from the packed register, v_cvt_pk_f16_f32 of the remainders: 4 VALU per pair),
 // for values that come from or go to MFMAs: hipcc inserts the MFMA hazard waits itself.
@@ -149,6 +176,12 @@ bool conv_halo_forward(hipStream_t s, const View& out, const View& in0, const Vi
 // the geometry is not covered), and the activation-range flag (|v| >= 65504 seen).
 struct X3Tile { int bm, bn, ng; };
 X3Tile x3_tile(int ks, int cout);
+// A fragments per (step, m32) in the packed direct-conv weights: hi, lo, and for 7x7 also
+// hi * 2^-11 (the weight side of the scaled-lo product, read from LDS instead of 4
+// v_pk_mul_f16 per fragment: the 7x7 tile reuses each A fragment for one MFMA triple only,
+// and its one workgroup per CU has the LDS to spare; the 3x3 / 1x1 tiles would lose their
+// second workgroup per CU)
+constexpr int x3_afrags(int ks) { return ks == 7 ? 3 : 2; }
 // With epi.stats set, *stats_slots receives the number of partial slots per (b, group)
 // the epilogue wrote (0: not computed, the caller runs the statistics pass).
 bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
@@ -261,8 +294,8 @@ bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& 
 // init_conv's x-branch composed with init_noise_conv into 49 border-class 13x13
 // kernels (xpath_x3.hip): out[:, :Cout] = sum_c K_c * x + cbias_c for the 3-channel x
 struct XPathArgs {
-  const float* x; long xb, xc, xt;
-  int T, L, F;
+  const float* x; long xb, xc, xt;  // the zero-padded copy (xpad_forward)
+  int T, L, F, LP;
   float* out; long ob, oc, ot; int Cout;
   const _Float16* w; const float* rscale; const float* cbias;
   int* range;
@@ -270,10 +303,14 @@ struct XPathArgs {
 };
 bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
                       const float* cbias);
+// the zero-padded copy of the 3-channel x both kernels above read: [B][3][T][LP][LP], x at
+// (6, 6), LP = xpad_size(L)
+int xpad_size(int L);
+void xpad_forward(hipStream_t s, const View& xpad, const View& x);
 // maxpool(1,2,2)(init_noise_conv(x)) in one kernel (xpath_x3.hip): out [B][C][T][L/2][L/2]
 struct NoisePoolArgs {
-  const float* x; long xb, xc, xt;
-  int T, L, F;
+  const float* x; long xb, xc, xt;  // the zero-padded copy (xpad_forward)
+  int T, L, F, LP;
   float* out; long ob, oc, ot; int Cout;
   const _Float16* w; const float* rscale; const float* bias;
   int* range;

@@ -348,7 +348,7 @@ __global__ __launch_bounds__(256) void gn_apply_x3op_kernel(const float* __restr
       bad |= fabsf(w) >= 65504.f;
       const _Float16 a = (_Float16)w;
       hi[e >> 3][e & 7] = a;
-      lo[e >> 3][e & 7] = (_Float16)(w - (float)a);
+      lo[e >> 3][e & 7] = (_Float16)((w - (float)a) * X3_LO_UP);  // scaled lo (split2s, kernels.h)
     }
     if (tpos < n) {
       _Float16* d = ob + (long)tpos * 8;

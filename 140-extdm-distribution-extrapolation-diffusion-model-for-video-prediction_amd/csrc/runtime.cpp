@@ -219,7 +219,8 @@ struct ExtdmHandle {
     const X3Tile tl = x3_tile(ks, co);
     const int cib = 16 * tl.ng, ncgb = (ci + cib - 1) / cib, mt = (co + tl.bm - 1) / tl.bm;
     const int m32 = tl.bm / 32, steps = tl.ng * ks;
-    const size_t ah = (size_t)steps * m32 * 2 * 512;
+    const int af = x3_afrags(ks);  // hi, lo (, hi * 2^-11)
+    const size_t ah = (size_t)steps * m32 * af * 512;
     std::vector<float> scale(co), rs(co);
     for (int m = 0; m < co; ++m) {
       float mx = 0.f;
@@ -244,9 +245,10 @@ struct ExtdmHandle {
                     const float v = w[((size_t)m * ci + c) * kk + ky * ks + kx] * scale[m];
                     const _Float16 hi = (_Float16)v;
                     const _Float16 lo = (_Float16)(v - (float)hi);
-                    const size_t base = (((((size_t)mtile * ncgb + cb) * ks + ky) * steps + g * ks + kx) * m32 + q) * 2;
+                    const size_t base = (((((size_t)mtile * ncgb + cb) * ks + ky) * steps + g * ks + kx) * m32 + q) * af;
                     a[(base + 0) * 512 + l * 8 + e] = hi;
                     a[(base + 1) * 512 + l * 8 + e] = lo;
+                    if (af == 3) a[(base + 2) * 512 + l * 8 + e] = (_Float16)((float)hi * (1.f / X3_LO_UP));
                   }
     pw.wx = dmalloc(a.size() * sizeof(_Float16));
     HIPCHK(hipMemcpy(pw.wx, a.data(), a.size() * sizeof(_Float16), hipMemcpyHostToDevice));
@@ -615,8 +617,9 @@ struct ExtdmHandle {
   // last window along a shifted dim d, the only one whose tokens carry two labels — and
   // each class has its own table; an unshifted layer has one.
   static int region_label(int c, int P, int w, int s) { return s == 0 ? 2 : c >= P - s ? 2 : c >= P - w ? 1 : 0; }
-  const float* stw_mask_bias(const std::string& p, const AttnGeom& g, int& npat) {
-    const std::string key = p + "|" + std::to_string(g.ws0) + "," + std::to_string(g.ws1) + "," + std::to_string(g.ws2) +
+  // s2: the factor the kernel's scores carry (AttnX3W::s2), applied to bias and masks
+  const float* stw_mask_bias(const std::string& p, const AttnGeom& g, int& npat, float s2) {
+    const std::string key = p + "|" + std::to_string(std::ilogb(s2)) + "|" + std::to_string(g.ws0) + "," + std::to_string(g.ws1) + "," + std::to_string(g.ws2) +
                             "|" + std::to_string(g.ss0) + "," + std::to_string(g.ss1) + "," + std::to_string(g.ss2) +
                             "|" + std::to_string(g.Dp) + "," + std::to_string(g.Hp) + "," + std::to_string(g.Wp);
     auto it = mask_bias.find(key);
@@ -648,7 +651,7 @@ struct ExtdmHandle {
               v = bh.first[((size_t)hd * st + i) * st + j];
               if (shifted && lab[i] != lab[j]) v += -100.f;
             }
-            t[(((size_t)pat * nh + hd) * 32 + i) * 32 + j] = v;
+            t[(((size_t)pat * nh + hd) * 32 + i) * 32 + j] = v * s2;
           }
     }
     float* d = dmalloc(t.size() * 4);
@@ -658,8 +661,8 @@ struct ExtdmHandle {
   }
   // temporal attention (one table): T5 bias of (query frame, key frame), -inf for another
   // pixel's frames and for key frames >= D (32-token groups of 32 / per pixels)
-  const float* temporal_mask_bias(const AttnGeom& g) {
-    const std::string key = "temporal|" + std::to_string(g.D);
+  const float* temporal_mask_bias(const AttnGeom& g, float s2) {
+    const std::string key = "temporal|" + std::to_string(g.D) + "|" + std::to_string(std::ilogb(s2));
     auto it = mask_bias.find(key);
     if (it != mask_bias.end()) return it->second.first;
     const int nh = cfg.heads, per = g.D <= 16 ? 16 : 32;
@@ -670,7 +673,7 @@ struct ExtdmHandle {
         for (int j = 0; j < 32; ++j) {
           const int pi = i / per, ti = i % per, pj = j / per, tj = j % per;
           t[((size_t)hd * 32 + i) * 32 + j] =
-              (pi != pj || tj >= g.D) ? -INFINITY : time_bias_host[(size_t)hd * 1024 + ti * 32 + tj];
+              (pi != pj || tj >= g.D) ? -INFINITY : time_bias_host[(size_t)hd * 1024 + ti * 32 + tj] * s2;
         }
     float* d = dmalloc(t.size() * 4);
     HIPCHK(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
@@ -715,7 +718,9 @@ struct ExtdmHandle {
   // [hi|lo][lane][8] for q, k, v (row u*32 + lc, channels 16s + 8h + e) and the
   // projection (row ct*32 + lc, hid u*32 + 16s' + 8(e>>2) + 4h + (e&3): the row order
   // of the O^T accumulator). Each matrix is scaled by one power of two.
-  struct AttnX3W { void* w = nullptr; float* sc = nullptr; };
+  // sc: [q, k, v, proj factors, softmax exp2 factor] (stw_x3.hip kernel header); s2 =
+  // 2^(e_q + e_k), the factor of the scores (and of their bias / mask table)
+  struct AttnX3W { void* w = nullptr; float* sc = nullptr; float s2 = 1.f; };
   std::unordered_map<std::string, AttnX3W> attn_x3w;
   static float pow2_scale(const float* p, size_t n, float& inv) {
     float mx = 0.f;
@@ -725,7 +730,16 @@ struct ExtdmHandle {
     inv = std::ldexp(1.f, -e);
     return std::ldexp(1.f, e);
   }
-  const AttnX3W& packed_attn_x3(const std::string& nqkv, const std::string& nproj) {
+  // ng / nb: the affine of the norm whose output the kernel splits (MODE 0: the PreNorm
+  // gamma; MODE 1: the inner LayerNorm's weight and bias; nb empty without a bias)
+  static int pow2_exp(double v) {  // e with v * 2^e in [1, 2), clamped; 0 for v == 0
+    if (!(v > 0.0) || !std::isfinite(v)) return 0;
+    int e = 0;
+    std::frexp(v, &e);
+    return std::min(30, std::max(-30, 1 - e));
+  }
+  const AttnX3W& packed_attn_x3(const std::string& nqkv, const std::string& nproj, const std::string& ng,
+                                const std::string& nb) {
     auto it = attn_x3w.find(nqkv);
     if (it != attn_x3w.end()) return it->second;
     const HostTensor& tq = H(nqkv);
@@ -762,11 +776,48 @@ struct ExtdmHandle {
               put(ub + ((size_t)3 * KS + ct * 2 + s2) * 1024, l, e, tp.f[(size_t)c * hid + hd] * sc[3]);
             }
     }
+    // Operand exponents (stw_x3.hip kernel header). Relative to a split input of largest
+    // |value| in [1, 2) (the kernel's 2^e_w carries a further 2^8, folded back through the
+    // factors below); channel c of it is then ~ (|g_c| + |b_c|) * 2^e_x / 4 (e_x
+    // brings the largest affine to [1, 2); a unit-variance z peaks near 4). e_q / e_k / e_v
+    // bring the largest expected row norm of q * q_scale, k, v (weights times those channel
+    // scales) to [1, 2). Powers of two: the scaling itself is exact.
+    const HostTensor& tg = H(ng);
+    REQUIRE((int)tg.f.size() == C, "attention norm affine size: " + ng);
+    std::vector<double> sx(C);
+    double mx = 0.0;
+    for (int c = 0; c < C; ++c) {
+      sx[c] = std::fabs((double)tg.f[c]) + (nb.empty() ? 0.0 : std::fabs((double)H(nb).f[c]));
+      mx = std::max(mx, sx[c]);
+    }
+    const int ex = pow2_exp(mx);
+    int em[3];
+    for (int m = 0; m < 3; ++m) {
+      double best = 0.0;
+      for (int d = 0; d < hid; ++d) {
+        double n2 = 0.0;
+        for (int c = 0; c < C; ++c) {
+          const double w = (double)tq.f[((size_t)m * hid + d) * C + c] * std::ldexp(sx[c], ex) * 0.25;
+          n2 += w * w;
+        }
+        best = std::max(best, std::sqrt(n2));
+      }
+      // to [2^4, 2^5) for q and k, [2^2, 2^3) for v: values down to 2^-7 / 2^-5 of the typical
+      // one keep a normal lo, with headroom to 65504 (O = P' v' <= 16 max|v'| with P' = 16 P)
+      em[m] = pow2_exp(best * (m == 0 ? (double)q_scale() : 1.0)) + (m < 2 ? 4 : 2);
+    }
+    float scv[5];
+    scv[0] = std::ldexp(inv[0], em[0]);
+    scv[1] = std::ldexp(inv[1], em[1]);
+    scv[2] = std::ldexp(inv[2], em[2]);
+    scv[3] = std::ldexp(inv[3], -(em[2] + 4));
+    scv[4] = (float)std::ldexp(1.4426950408889634, -(em[0] + em[1]));
     AttnX3W r;
+    r.s2 = std::ldexp(1.f, em[0] + em[1]);
     r.w = dmalloc(a.size() * sizeof(_Float16));
     HIPCHK(hipMemcpy(r.w, a.data(), a.size() * sizeof(_Float16), hipMemcpyHostToDevice));
-    r.sc = dmalloc(4 * sizeof(float));
-    HIPCHK(hipMemcpy(r.sc, inv, 4 * sizeof(float), hipMemcpyHostToDevice));
+    r.sc = dmalloc(5 * sizeof(float));
+    HIPCHK(hipMemcpy(r.sc, scv, 5 * sizeof(float), hipMemcpyHostToDevice));
     return attn_x3w[nqkv] = r;
   }
   // f16x3 convolutions (F16X3, and BF16_ATTN, whose attention core alone is bf16)
@@ -823,9 +874,9 @@ struct ExtdmHandle {
     }
     if (fused_x3) {
       const std::string a = p + ".fn.fn.attn";
-      const AttnX3W& w = packed_attn_x3(a + ".qkv.weight", a + ".proj.weight");
+      const AttnX3W& w = packed_attn_x3(a + ".qkv.weight", a + ".proj.weight", p + ".fn.norm.gamma", "");
       int npat = 1;
-      const float* mb = stw_mask_bias(p, g, npat);
+      const float* mb = stw_mask_bias(p, g, npat, w.s2);
       if (plan) return;
       REQUIRE(stw_x3(s, x, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), w.w, w.sc, D(a + ".proj.bias"),
                      mb, npat, rope_cos, rope_sin, q_scale()),
@@ -881,11 +932,13 @@ struct ExtdmHandle {
       return;
     }
     if (fused_x3) {
-      const AttnX3W& w = packed_attn_x3(a + ".attn.to_qkv.weight", a + ".attn.to_out.weight");
-      const float* mb = temporal_mask_bias(g);
+      const AttnX3W& w = packed_attn_x3(a + ".attn.to_qkv.weight", a + ".attn.to_out.weight", a + ".norm.weight",
+                                        a + ".norm.bias");
+      const float* mb = temporal_mask_bias(g, w.s2);
       if (plan) return;
       REQUIRE(temporal_x3(s, x, out, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), D(a + ".norm.weight"),
-                          D(a + ".norm.bias"), w.w, w.sc, mb, rope_cos, rope_sin, q_scale()),
+                          D(a + ".norm.bias"), w.w, w.sc, mb,
+                          rope_cos, rope_sin, q_scale()),
               "f16x3 temporal attention launch rejected");
       return;
     }
@@ -1119,6 +1172,12 @@ struct ExtdmHandle {
           x0p = alloc_cf(B, 256, tp, L, L);
           conv(x0p, vx, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
         }
+        // the zero-padded copy of x the composed x-branch and the fused noise_pool gather from
+        View xpad;
+        if (xp || (arch == EXTDM_ARCH_U12 && !x0p.p)) {
+          xpad = alloc_cf(B, 3, tp, xpad_size(L), xpad_size(L));
+          if (!plan) xpad_forward(s, xpad, vx);
+        }
         View fu;
         if (arch == EXTDM_ARCH_U12) {
           REQUIRE(L / 2 == fs, "TrajWarp: maxpooled latent must match cond_fea size");
@@ -1128,7 +1187,7 @@ struct ExtdmHandle {
           } else {
             const XPathW& nw = Pnoise_pool();
             if (!plan)
-              REQUIRE(noise_pool_x3_forward(s, xq, vx, nw.w, nw.rs, D("init_noise_conv.bias")),
+              REQUIRE(noise_pool_x3_forward(s, xq, xpad, nw.w, nw.rs, D("init_noise_conv.bias")),
                       "fused init_noise_conv + maxpool launch rejected");
           }
           View fp2 = alloc_cf(B, cfg.fea_ch, tp, fs, fs);
@@ -1141,7 +1200,7 @@ struct ExtdmHandle {
         if (xp) {
           // rp = K_class * x + cbias_class (x-branch + both biases), then rp += Wb * pad(fu)
           const XPathW& xw = Pxpath();
-          if (!plan) REQUIRE(xpath_x3_forward(s, rp, vx, xw.w, xw.rs, xw.cb), "composed init_conv launch rejected");
+          if (!plan) REQUIRE(xpath_x3_forward(s, rp, xpad, xw.w, xw.rs, xw.cb), "composed init_conv launch rejected");
           conv(rp, fu, nullptr, P("init_conv.weight#fea"), 1, 3, nullptr, &rp);
         } else {
           conv(rp, x0p, &fu, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
@@ -2007,6 +2066,47 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     // layers 6-8: the attention launches of the forward, timed the same way: 6 = level-0
     // shifted STW attention (downs.0.1, in place on x), 7 = init_temporal_attn (x -> out),
     // 8 = the TrajWarp cross-attention core over the pre-split cond-frame K / V (u12:719-773).
+    // layers 9-10: the low-K gathers of the x-branch over the tp frames, from the zero-padded
+    // copy of x (xpad_forward, written once untimed): 9 = the composed 13x13 init_conv
+    // x-branch (xpath_x3.hip), 10 = init_noise_conv + maxpool (noise_pool_x3).
+    if (layer == 9 || layer == 10) {
+      REQUIRE(h->x3_convs() && h->xpath_enabled(), "bench layers 9-10: the f16x3 x-branch is off");
+      const int tp = h->cfg.tp, LP = xpad_size(L);
+      View x = h->alloc_cf(B, 3, tp, L, L), xp = h->alloc_cf(B, 3, tp, LP, LP);
+      fill_normal(s, x.p, 1, (int)x.numel(), 17, 0, 0, 6);
+      xpad_forward(s, xp, x);
+      double flop = 0;
+      std::function<void()> launch;
+      if (layer == 9) {
+        const auto& xw = h->Pxpath();
+        View r = h->alloc_cf(B, h->cfg.dim, tp, L, L);
+        flop = (double)B * tp * L * L * 2.0 * 3 * 169 * h->cfg.dim;
+        launch = [&, r, xp] { REQUIRE(xpath_x3_forward(s, r, xp, xw.w, xw.rs, xw.cb), "bench layer 9: launch rejected"); };
+      } else {
+        REQUIRE(h->cfg.arch == EXTDM_ARCH_U12, "bench layer 10: no TrajWarp (u12 only)");
+        const auto& nw = h->Pnoise_pool();
+        View q = h->alloc_cf(B, 256, tp, L / 2, L / 2);
+        flop = (double)B * tp * L * L * 2.0 * 3 * 49 * 256;
+        launch = [&, q, xp] {
+          REQUIRE(noise_pool_x3_forward(s, q, xp, nw.w, nw.rs, h->D("init_noise_conv.bias")), "bench layer 10: launch rejected");
+        };
+      }
+      launch();
+      hipEvent_t e0, e1;
+      HIPCHK(hipEventCreate(&e0));
+      HIPCHK(hipEventCreate(&e1));
+      HIPCHK(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; ++i) launch();
+      HIPCHK(hipEventRecord(e1, s));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      *ms_out = ms / iters;
+      *flops_out = flop;
+      return;
+    }
     if (layer >= 6 && layer <= 8) {
       const int C = h->cfg.dim;
       double flop = 0;

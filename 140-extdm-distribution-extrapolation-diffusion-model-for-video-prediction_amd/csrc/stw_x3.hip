@@ -147,8 +147,8 @@ struct UnitLayout {
 // pixel's frames (MODE 1). MODE 0 shifted layers carry 8 window classes (bit d: last
 // window along a shifted dim, where the region labels differ), the rest one. A lane's 16
 // score registers hold keys j = dof(r, h) = 8q + 4h + e (r = 4q + e): four 16-B rows of
-// its query's table row, loaded straight into the score accumulator that the QK^T
-// MFMAs then add to — no VALU for bias or masks.
+// its query's table row, added to the QK^T accumulator in one v_add per score (masks need
+// no further VALU). The table carries the scores' factor 2^(e_q + e_k) (wsc note).
 template <int C, int MODE, int DH, int NW, bool TILE>
 // x and out alias for the in-place STW layers (MODE 0): no __restrict__ on them.
 __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float* out,
@@ -192,7 +192,17 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   };
 
 
-  const float sq = wsc[0] * q_scale, sk = wsc[1], sv = wsc[2];
+  // Operand scales. An fp16 lo below 2^-14 is subnormal, so a split operand far below unit
+  // scale loses bits (tests/test_gpu_precision.py activation-scale cases); here every split
+  // operand is brought near unit scale by powers of two (exact): the normalised input by
+  // 2^e_w, e_w from the workgroup's largest |value| (prologue), and wsc (packed_attn_x3,
+  // runtime.cpp) takes the MFMA results (weights pre-scaled per matrix) to q * q_scale *
+  // 2^e_q, k * 2^e_k, v * 2^e_v once 2^-e_w is folded in, exponents estimated from the
+  // weights and the norm's affine for an input of unit largest value;
+  // the scores are then S * 2^(e_q + e_k) (the bias / mask table carries the same factor),
+  // csm = log2(e) * 2^-(e_q + e_k) is the softmax's exp2 factor, P is split as 16 P (its lo
+  // normal down to P ~ 2^-7) and spj undoes 2^(e_v + 4) with the projection's weight scale
+  const float sq0 = wsc[0] * q_scale, sk0 = wsc[1], sv0 = wsc[2], csm = wsc[4];
   constexpr bool FOLD = C == 64;
 
   const int h = lane >> 5, lc = lane & 31;
@@ -221,7 +231,22 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       __builtin_amdgcn_global_load_lds((const void*)(src + pc * 512 + lane * 8), (lds_ptr_t)(dst + pc * 512), 16, 0, 0);
     }
   };
-  load_unit(0, wsm);
+  // PIPE: step j's slot = the q / k / v pieces of unit j and the proj pieces of unit j - 1
+  // (pieces pc = wave + i * NW: the first 3 * KS pieces are q, k, v, the rest proj)
+  constexpr bool PIPE = false;  // C == 64: measured 3-4 % slower than one unit per step (kept for A/B)
+  auto load_step = [&](int j, _Float16* dst) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < UL::HALVES / 512 / NW; ++i) {
+      const int pc = wave + i * NW;
+      const bool is_qkv = pc < 3 * KS * 2;  // wave-uniform; static per (i, wave range)
+      const int u = is_qkv ? j : j - 1;
+      if (u < 0 || u >= UNITS) continue;
+      __builtin_amdgcn_global_load_lds((const void*)(wpk + (long)u * UL::HALVES + pc * 512 + lane * 8),
+                                       (lds_ptr_t)(dst + pc * 512), 16, 0, 0);
+    }
+  };
+  if (PIPE) load_step(0, wsm);
+  else load_unit(0, wsm);
 
   // ---- MODE 0 tile path (template TILE, host check attn_x3_tile_ok): the workgroup's 8 windows
   // are one row of 2x4x4 windows across W = 32 (no padding), so together they read
@@ -295,7 +320,9 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   const int vpro = tok_ok ? (int)((8 * h * sc + me.pos) * 4) : OOB;  // channel 8h + (16k + e)
   int bad = 0;
   h8 xh[KS], xl[KS];
-  float m1 = 0.f, den1 = 1.f, rden1 = 1.f;
+  float m1 = 0.f, den1 = 1.f, rden1 = 1.f, gi = 1.f;
+  // e_w reduction slots (NW floats) behind everything else the kernel keeps in LDS
+  float* const redL = reinterpret_cast<float*>(wsm + 2 * UL::HALVES) + (TILE || PIPE ? C * 256 + 128 + 2048 : 0);
   {
     float xv[KS][8];
     float s = 0.f;
@@ -356,8 +383,45 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
           xv[k][e] = ((xv[k][e] - m2) * rstd2 * ldb(rs_lw, 32 * h, (16 * k + e) * 4) +
                       ldb(rs_lb, 32 * h, (16 * k + e) * 4)) * vm;
     }
+    // e_w: the workgroup's largest |normalised value| to [2^8, 2^9) (a LayerNorm whose variance
+    // is below its eps leaves the output far from unit scale, so this is data-dependent);
+    // one barrier, which also retires every wave's tile reads before PIPE reuses the tile
+    float am = 0.f;
 #pragma unroll
-    for (int k = 0; k < KS; ++k) split8(xv[k], xh[k], xl[k], bad);
+    for (int k = 0; k < KS; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(xv[k][e]));
+    am = xh_max(am);
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) am = fmaxf(am, __shfl_xor(am, off));
+    if (lane == 0) redL[wave] = am;
+    __syncthreads();
+    float wm = redL[0];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) wm = fmaxf(wm, redL[i]);
+    // largest at [2^8, 2^9): every value above 2^-11 of it keeps a normal lo
+    int ew = wm > 0.f && wm < INFINITY ? 9 - __builtin_amdgcn_frexp_expf(wm) : 0;
+    ew = ew < -100 ? -100 : (ew > 100 ? 100 : ew);
+    const float gs = __builtin_amdgcn_ldexpf(1.f, ew);
+    gi = __builtin_amdgcn_ldexpf(1.f, -ew);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[k][e] *= gs;
+      split8(xv[k], xh[k], xl[k], bad);
+    }
+  }
+  const float sq = sq0 * gi, sk = sk0 * gi, sv = sv0 * gi;
+  // PIPE: the normalised fragments go to LDS ([wave][k-step][hi|lo][lane][8], 8 KB per wave,
+  // in the tile's place — every wave must be done reading the tile first) and are re-read
+  // per unit: the 32 VGPRs they held are what the two units in flight need
+  h8* const xfr = reinterpret_cast<h8*>(tileT) + wave * (KS * 2 * 64);
+  if (PIPE) {
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      xfr[(2 * k) * 64 + lane] = xh[k];
+      xfr[(2 * k + 1) * 64 + lane] = xl[k];
+    }
   }
   stamp(22);
 
@@ -383,7 +447,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   // lanes] and are re-read per unit (8 conflict-free ds_read_b128) instead of holding 32
   // VGPRs through the unit loop
   float4* const ropeL = reinterpret_cast<float4*>(tileT + C * 256 + 128);
-  if (TILE && wave == 0) {
+  if ((TILE || PIPE) && wave == 0) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       ropeL[(0 + j) * 64 + lane] = make_float4(rcq[4 * j], rcq[4 * j + 1], rcq[4 * j + 2], rcq[4 * j + 3]);
@@ -443,7 +507,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     // follows in program order and does not depend on V) between them
     v_mfma(W, v);
   };
-  // the bias / mask rows of unit u's heads (straight into the score accumulators)
+  // the bias / mask rows of unit u's heads (added to the scores in attend)
   auto load_bias = [&](int u, f32x16* bia) __attribute__((always_inline)) {
 #pragma unroll
     for (int hh = 0; hh < HPU; ++hh)
@@ -457,7 +521,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   // scale + RoPE of q, k; the unit's heads: S^T = bias + K Q^T (rows = keys j, lane =
   // query i), softmax, O^T = V^T P^T
   auto attend = [&](f32x16& q, f32x16& k, const f32x16& v, const f32x16* bia) __attribute__((always_inline)) {
-    if (TILE) {
+    if (TILE || PIPE) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const float4 a = ropeL[(0 + j) * 64 + lane], bq = ropeL[(2 + j) * 64 + lane];
@@ -496,24 +560,31 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     for (int r = 0; r < 16; ++r) o[r] = 0.f;
 #pragma unroll
     for (int hh = 0; hh < HPU; ++hh) {
-      f32x16 sc_ = bia[hh];
+      // K Q^T from zero, then the bias / mask in one add: accumulated onto the bias, every
+      // MFMA of the chain rounded at the bias's ulp (one rounding, as the reference's
+      // qk^T + bias, where the bias dominates small activations)
+      f32x16 sc_;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc_[r] = 0.f;
 #pragma unroll
       for (int s = 0; s < 2; ++s)
         if (HPU == 1 || s == hh) sc_ = mma3(kf[s][0], kf[s][1], qf[s][0], qf[s][1], sc_);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc_[r] += bia[hh][r];
       float mx = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc_[r]);
       mx = xh_max(mx);
       // exp(s - mx) as v_exp_f32 (2^x) of fma(s, log2 e, -mx log2 e): masked -inf -> 0
-      const float mxl = mx * 1.44269504088896341f;
+      const float mxl = mx * csm;
       float sum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        sc_[r] = __builtin_amdgcn_exp2f(fmaf(sc_[r], 1.44269504088896341f, -mxl));
+        sc_[r] = __builtin_amdgcn_exp2f(fmaf(sc_[r], csm, -mxl));
         sum += sc_[r];
       }
       sum = xh_sum(sum);
-      const float inv = 1.f / sum;
+      const float inv = 16.f / sum;  // P * 2^4 (wsc header note)
 #pragma unroll
       for (int r = 0; r < 16; ++r) sc_[r] *= inv;
       // O^T[dd][i] = sum_j V^T[dd][j] P^T[j][i]; lanes of the unit's other head masked
@@ -562,6 +633,58 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   stamp(1);
   if (dbg & 16) {
     // timing only: no unit loop (prologue + epilogue cost)
+  } else if (PIPE) {
+    // Software-pipelined units (C = 64, two waves per SIMD): step j runs the qkv MFMAs of
+    // unit j beside the RoPE / splits / softmax / PV / projection of unit j - 1, so the
+    // MFMA pipe has independent work while the attention VALU runs (with one unit per step
+    // both waves of a SIMD reached their VALU phases together and the pipe idled). Ring
+    // slot j holds [qkv(j) | proj(j - 1)] (load_step), so two 32-KB slots still suffice.
+    f32x16 q, k, v;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { q[r] = 0.f; k[r] = 0.f; v[r] = 0.f; }
+#pragma unroll
+    for (int j = 0; j <= UNITS; ++j) {
+      _Float16* W = wsm + (j & 1) * UL::HALVES;
+      unit_barrier(j);
+      f32x16 bia[HPU];
+      if (j >= 1) load_bias(j - 1, bia);
+      if (j + 1 <= UNITS) load_step(j + 1, wsm + ((j + 1) & 1) * UL::HALVES);
+      if (TILE && j == UNITS) {
+        // the x tile again for the residual epilogue, into the fragments' place (no wave reads
+        // them after step UNITS - 1): in flight during the last unit's attention
+        const int r = lane >> 3, qq = (lane & 7) ^ r;
+        int roff = trow[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) roff = r == i ? trow[i] : roff;
+#pragma unroll
+        for (int i = 0; i < C / NW; ++i) {
+          const int c = wave + i * NW;
+          __builtin_amdgcn_global_load_lds((const void*)(xb + (long)c * sc + roff + 4 * qq),
+                                           (lds_ptr_t)(tileT + c * 256), 16, 0, 0);
+        }
+      }
+      f32x16 qn, kn, vn;
+      if (j < UNITS) {
+        // per k-step: the wave's X fragments from LDS, then q, k, v's three MFMAs each
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { qn[r] = 0.f; kn[r] = 0.f; vn[r] = 0.f; }
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const h8 xhs = xfr[(2 * s) * 64 + lane], xls = xfr[(2 * s + 1) * 64 + lane];
+          const _Float16* fq = W + UL::Q + s * UL::FRAG + lane * 8;
+          const _Float16* fk = W + UL::K + s * UL::FRAG + lane * 8;
+          const _Float16* fv = W + UL::V + s * UL::FRAG + lane * 8;
+          qn = mma3(*reinterpret_cast<const h8*>(fq), *reinterpret_cast<const h8*>(fq + 512), xhs, xls, qn);
+          kn = mma3(*reinterpret_cast<const h8*>(fk), *reinterpret_cast<const h8*>(fk + 512), xhs, xls, kn);
+          vn = mma3(xhs, xls, *reinterpret_cast<const h8*>(fv), *reinterpret_cast<const h8*>(fv + 512), vn);
+        }
+      }
+      if (j >= 1) {
+        const f32x16 o = attend(q, k, v, bia);
+        proj(W, o);
+      }
+      if (j < UNITS) { q = qn; k = kn; v = vn; }
+    }
   } else {
     for (int u = 0; u < UNITS; ++u) {
       _Float16* W = wsm + (u & 1) * UL::HALVES;
@@ -584,6 +707,10 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     }
   }
   stamp(18);
+  if (TILE && PIPE && !(dbg & 16)) {  // the re-loaded x tile (every wave's pieces) has landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   // the loop's splits: one finite check of the token's accumulators (see split8)
   {
     float chk = 0.f;
@@ -705,7 +832,12 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
   const size_t ring = (size_t)2 * UnitLayout<C>::HALVES * sizeof(_Float16);
   const bool tile = MODE == 0 && C == 64 && NW == 8 && attn_x3_tile_ok(x, out, g, groups);
   size_t lds = (MODE == 1 && C == 64 && NW == 8) ? std::max(ring, (size_t)C * 328 * sizeof(float)) : ring;
-  if (tile) lds = ring + ((size_t)C * 8 * 32 + 2 * 64 + 8 * 64 * 4) * sizeof(float);
+  // tile / PIPE (C = 64): behind the ring the x tile or the normalised fragments (C * 256
+  // floats), gamma + proj bias (128), the RoPE factors (8 x 64 float4)
+  if (tile || C == 64) lds = std::max(lds, ring + ((size_t)C * 8 * 32 + 2 * 64 + 8 * 64 * 4) * sizeof(float));
+  // + the e_w reduction slots (MODE 1's epilogue staging may overlap them: dead by then)
+  lds = std::max(lds, ring + (size_t)((tile || C == 64) ? C * 8 * 32 + 2 * 64 + 8 * 64 * 4 : 0) * sizeof(float) +
+                          NW * sizeof(float));
   // per device, once: the dynamic-LDS limit
   static std::once_flag once[64];
   int dev = 0;

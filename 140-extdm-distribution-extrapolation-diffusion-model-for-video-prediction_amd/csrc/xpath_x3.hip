@@ -34,7 +34,7 @@ constexpr int KSTEPS = 3 * 13;  // (ci, dy); 16 dx columns per step
 
 __device__ __forceinline__ f32x16 mma3(const h8& ah, const h8& al, const h8& bh, const h8& bl, f32x16 c) {
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(lo_dn(ah), bl, c, 0, 0, 0);  // scaled x lo (gather8)
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
   return c;
 }
@@ -57,8 +57,48 @@ __device__ __forceinline__ void gather8(const float* plane, int y, int xs, int L
     bad |= fabsf(v) >= 65504.f;
     const _Float16 hi = (_Float16)v;
     bh[e] = hi;
-    bl[e] = (_Float16)(v - (float)hi);
+    bl[e] = (_Float16)((v - (float)hi) * X3_LO_UP);  // scaled lo (split2s, kernels.h)
   }
+}
+
+// hi / lo' fragments of 8 consecutive values of a row of the zero-padded copy of x (xpad_kernel):
+// two 16-B loads (dword alignment suffices for global_load_dwordx4) and no per-element index,
+// clamp or mask VALU (the round-2 gather8 spent ~10 VALU per value on them: 158 VALU per 12
+// MFMAs in xpath's k-loop). Columns the composed kernels do not use (dx >= 13, noise_pool's
+// 8th column) are read from the padding or the next columns and meet zero weights: the
+// values are finite, so their products are exact zeros. Compiler-visible split (the
+// fragments feed MFMAs directly; kernels.h split2 note), lo scaled by 2^11 (split2s).
+__device__ __forceinline__ void gather8p(const float* p, h8& bh, h8& bl, float& am) {
+  const float4 u = *reinterpret_cast<const float4*>(p);
+  const float4 w = *reinterpret_cast<const float4*>(p + 4);
+  const float v[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+  // lo' = fp16(fma(hi, -2^11, 2^11 v)): v * 2^11 exact, the fma exact (hi agrees with v in
+  // its leading 11 bits), one rounding; hi enters the v_fma_mix as its fp16 register
+  const float up = split_src(X3_LO_UP);
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const float v0 = split_src(v[e]), v1 = split_src(v[e + 1]);
+    amax2(am, v0, v1);  // loaded values, not MFMA results: the asm form is hazard-free here
+    const f16x2_t hh = __builtin_convertvector((f32x2_t){v0, v1}, f16x2_t);
+    bh[e] = hh.x; bh[e + 1] = hh.y;
+    bl[e] = (_Float16)__builtin_fmaf((float)hh.x, -up, v0 * up);
+    bl[e + 1] = (_Float16)__builtin_fmaf((float)hh.y, -up, v1 * up);
+  }
+}
+
+// x [B][3][T][L][L] -> xpad [B][3][T][LP][LP] with x at (6, 6) and zeros around (LP >= L + 16:
+// xpath reads rows py - 6 .. py + 6 and columns px - 6 .. px + 9, noise_pool rows 2yp - 3 ..
+// 2yp + 5 and columns lc - 3 .. lc + 4)
+__global__ __launch_bounds__(256) void xpad_kernel(const float* __restrict__ x, long xb, long xc, long xt,
+                                                   float* __restrict__ xp, int T, int L, int LP, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int col = (int)(i % LP), row = (int)((i / LP) % LP);
+  const long pl = i / ((long)LP * LP);  // (b, ci, t)
+  const int t = (int)(pl % T), ci = (int)((pl / T) % 3);
+  const long b = pl / (3L * T);
+  const int y = row - 6, xx = col - 6;
+  xp[i] = (y >= 0 && y < L && xx >= 0 && xx < L) ? x[b * xb + ci * xc + t * xt + (long)y * L + xx] : 0.f;
 }
 
 __device__ __forceinline__ void class_span(int c, int L, int& start, int& count) {
@@ -95,7 +135,7 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
     const int b = f / a.T, t = f - b * a.T;
     py[nt] = y0 + iy;
     px[nt] = x0 + ix;
-    xoff[nt] = (long)b * a.xb + (long)t * a.xt;
+    xoff[nt] = (long)b * a.xb + (long)t * a.xt + (long)py[nt] * a.LP + px[nt];  // padded: row py + dy, col px + 8h
     ooff[nt] = (long)b * a.ob + (long)t * a.ot + (long)py[nt] * L + px[nt];
   }
 
@@ -108,10 +148,11 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
       for (int r = 0; r < 16; ++r) acc[m][nt][r] = 0.f;
 
   const _Float16* wc = a.w + (long)cls * KSTEPS * M32 * 1024 + lane * 8;
-  int bad = 0;
+  float am = 0.f;
   for (int ci = 0; ci < 3; ++ci) {
-    const float* xc = a.x + (long)ci * a.xc;
-#pragma unroll 1
+    const float* xc = a.x + (long)ci * a.xc + 8 * h;
+    // whole rows unrolled: the next k-steps' x / weight loads issue ahead of this one's MFMAs
+#pragma unroll
     for (int dy = 0; dy < 13; ++dy) {
       const int ks = ci * 13 + dy;
       h8 ah[M32], al[M32];
@@ -123,15 +164,14 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
       }
       h8 bh[2], bl[2];
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-        gather8(xc + xoff[nt], py[nt] + dy - 6, px[nt] + 8 * h - 6, L, h ? 5 : 8, ok[nt], bh[nt], bl[nt], bad);
+      for (int nt = 0; nt < 2; ++nt) gather8p(xc + xoff[nt] + dy * a.LP, bh[nt], bl[nt], am);
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
         for (int m = 0; m < M32; ++m) acc[m][nt] = mma3(ah[m], al[m], bh[nt], bl[nt], acc[m][nt]);
     }
   }
-  if (bad) atomicOr(a.range, 1);
+  if (am >= 65504.f) atomicOr(a.range, 1);
 
   // ---- epilogue (C/D map: col = lane & 31, row = (r&3) + 8(r>>2) + 4h) ----
   const float* rs = a.rscale + (long)cls * M32 * 32;
@@ -171,7 +211,8 @@ __global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
   const int f = rp / Lh, yp = rp - f * Lh;
   const int b = f / a.T, t = f - b * a.T;
   const bool ok = lc < L;
-  const float* xf = a.x + (long)b * a.xb + (long)t * a.xt;
+  // padded copy: row 2yp + nt + dy + 3, column lc + 3 (+ e)
+  const float* xf = a.x + (long)b * a.xb + (long)t * a.xt + (long)(2 * yp + 3) * a.LP + (ok ? lc : 0) + 3;
 
   f32x16 acc[MW][2];
 #pragma unroll
@@ -182,7 +223,7 @@ __global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
       for (int r = 0; r < 16; ++r) acc[m][nt][r] = 0.f;
   const _Float16* wq = a.w + (long)mq * MW * 1024 + lane * 8;
   const int M32 = (a.Cout + 31) / 32;
-  int bad = 0;
+  float am = 0.f;
 #pragma unroll 2
   for (int ks = 0; ks < 12; ++ks) {
     const int ci = ks / 4, dy = 2 * (ks % 4) + h;
@@ -195,14 +236,13 @@ __global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
     }
     h8 bh[2], bl[2];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-      gather8(xf + (long)ci * a.xc, 2 * yp + nt + dy - 3, lc - 3, L, dy < 7 ? 7 : 0, ok, bh[nt], bl[nt], bad);
+    for (int nt = 0; nt < 2; ++nt) gather8p(xf + (long)ci * a.xc + (nt + dy) * a.LP, bh[nt], bl[nt], am);
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int m = 0; m < MW; ++m) acc[m][nt] = mma3(ah[m], al[m], bh[nt], bl[nt], acc[m][nt]);
   }
-  if (bad) atomicOr(a.range, 1);
+  if (am >= 65504.f) atomicOr(a.range, 1);
   float* of = a.out + (long)b * a.ob + (long)t * a.ot + (long)yp * Lh + (lc >> 1);
 #pragma unroll
   for (int m = 0; m < MW; ++m)
@@ -217,14 +257,23 @@ __global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
 
 }  // namespace
 
+int xpad_size(int L) { return (L + 16 + 7) & ~7; }
+
+void xpad_forward(hipStream_t s, const View& xpad, const View& x) {
+  const long n = (long)x.B * 3 * x.T * xpad.H * xpad.W;
+  hipLaunchKernelGGL(xpad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x.p, x.sb, x.sc, x.st, xpad.p, x.T,
+                     x.H, xpad.W, n);
+}
+
+// x: the zero-padded copy (xpad_forward; LP = x.W, the latent L = out.H * 2)
 bool noise_pool_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
                            const float* bias) {
-  const int L = x.H;
-  if (x.C != 3 || x.W != L || L > 32 || (L & 1) || out.H != L / 2 || out.W != L / 2 || out.T != x.T ||
-      out.B != x.B || out.C % 128 != 0)
+  const int L = out.H * 2;
+  if (x.C != 3 || x.W != x.H || x.W != xpad_size(L) || x.st != (long)x.W * x.H || L > 32 || out.W != L / 2 ||
+      out.T != x.T || out.B != x.B || out.C % 128 != 0)
     return false;
   NoisePoolArgs a{};
-  a.x = x.p; a.xb = x.sb; a.xc = x.sc; a.xt = x.st;
+  a.x = x.p; a.xb = x.sb; a.xc = x.sc; a.xt = x.st; a.LP = x.W;
   a.T = x.T; a.L = L; a.F = x.B * x.T;
   a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
   a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.bias = bias; a.range = x3_range_ptr();
@@ -233,13 +282,15 @@ bool noise_pool_x3_forward(hipStream_t s, const View& out, const View& x, const 
   return true;
 }
 
+// x: the zero-padded copy (xpad_forward; LP = x.W, the latent L = out.H)
 bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
                       const float* cbias) {
-  const int L = x.H;
-  if (x.C != 3 || x.W != L || out.H != L || out.W != L || L < 7 || out.C > 64 || out.T != x.T || out.B != x.B)
+  const int L = out.H;
+  if (x.C != 3 || x.W != x.H || x.W != xpad_size(L) || x.st != (long)x.W * x.H || out.W != L || L < 7 ||
+      out.C > 64 || out.T != x.T || out.B != x.B)
     return false;
   XPathArgs a{};
-  a.x = x.p; a.xb = x.sb; a.xc = x.sc; a.xt = x.st;
+  a.x = x.p; a.xb = x.sb; a.xc = x.sc; a.xt = x.st; a.LP = x.W;
   a.T = x.T; a.L = L; a.F = x.B * x.T;
   a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
   a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.cbias = cbias; a.range = x3_range_ptr();
