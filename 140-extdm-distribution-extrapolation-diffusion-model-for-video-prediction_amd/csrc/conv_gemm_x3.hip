@@ -238,9 +238,11 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
+          // the scaled-lo product last: its lo_dn VALU is off the head of the chain (-3 %,
+          // interleaved A/B at B = 64)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[i], bl[j], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[i], bl[j], acc[i][j], 0, 0, 0);
         }
     }
     store_tile((kt & 1) ? As0 : As1, (kt & 1) ? Bs0 : Bs1);

@@ -118,8 +118,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   constexpr int CIB = 16 * NG;
   constexpr int MT32 = BM / 32;
   constexpr int STEPS = NG * KS;                // per A slot: (g, kx)
-  constexpr int AF = x3_afrags(KS);              // A fragments per (step, m32)
-  constexpr int AH = STEPS * MT32 * AF * 512;   // halves per ky slice
+  constexpr int AH = STEPS * MT32 * 2 * 512;    // halves per ky slice
   constexpr int AHS = KY * AH;                  // halves per A slot (stage)
   constexpr int STG = KS / KY;                  // stages per channel block
   static_assert(KS % KY == 0, "KY must divide KS");
@@ -400,11 +399,10 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
         h8 ah[TM], al[TM], ad[TM], bh[TN], bl[TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const _Float16* ap = As + ((step * MT32 + wm * TM + i) * AF) * 512 + lane * 8;
+          const _Float16* ap = As + ((step * MT32 + wm * TM + i) * 2) * 512 + lane * 8;
           ah[i] = *reinterpret_cast<const h8*>(ap);
           al[i] = *reinterpret_cast<const h8*>(ap + 512);
-          // pairs with the scaled activation lo (split2s, kernels.h)
-          ad[i] = AF == 3 ? *reinterpret_cast<const h8*>(ap + 1024) : lo_dn(ah[i]);
+          ad[i] = lo_dn(ah[i]);  // pairs with the scaled activation lo (split2s, kernels.h)
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -418,9 +416,11 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
+            // the scaled-lo product last: its lo_dn VALU is off the head of the chain (-3 %,
+            // interleaved A/B at B = 64)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[i], bl[j], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[i], bl[j], acc[i][j], 0, 0, 0);
           }
       }
     }
@@ -614,7 +614,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
           bool RGN = false, int SPL = 0>
 void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
-  constexpr int AH = KY * NG * KS * (BM / 32) * x3_afrags(KS) * 512;
+  constexpr int AH = KY * NG * KS * (BM / 32) * 2 * 512;
   const size_t xlo = XOP ? (size_t)((a.XPOS + 63) & ~63) * 16 : (size_t)a.XPOS * NG * 16;
   // + 32 halves (unused-slot dummy) + 2 * BM floats (epilogue scale / bias)
   const size_t lds = ((size_t)2 * AH + (size_t)XBUF * 2 * xlo + 32 + 4 * BM) * sizeof(_Float16);

@@ -176,12 +176,7 @@ bool conv_halo_forward(hipStream_t s, const View& out, const View& in0, const Vi
 // the geometry is not covered), and the activation-range flag (|v| >= 65504 seen).
 struct X3Tile { int bm, bn, ng; };
 X3Tile x3_tile(int ks, int cout);
-// A fragments per (step, m32) in the packed direct-conv weights: hi, lo, and for 7x7 also
-// hi * 2^-11 (the weight side of the scaled-lo product, read from LDS instead of 4
-// v_pk_mul_f16 per fragment: the 7x7 tile reuses each A fragment for one MFMA triple only,
-// and its one workgroup per CU has the LDS to spare; the 3x3 / 1x1 tiles would lose their
-// second workgroup per CU)
-constexpr int x3_afrags(int ks) { return ks == 7 ? 3 : 2; }
+
 // With epi.stats set, *stats_slots receives the number of partial slots per (b, group)
 // the epilogue wrote (0: not computed, the caller runs the statistics pass).
 bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,

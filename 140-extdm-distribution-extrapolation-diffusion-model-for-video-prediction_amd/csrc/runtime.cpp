@@ -219,8 +219,7 @@ struct ExtdmHandle {
     const X3Tile tl = x3_tile(ks, co);
     const int cib = 16 * tl.ng, ncgb = (ci + cib - 1) / cib, mt = (co + tl.bm - 1) / tl.bm;
     const int m32 = tl.bm / 32, steps = tl.ng * ks;
-    const int af = x3_afrags(ks);  // hi, lo (, hi * 2^-11)
-    const size_t ah = (size_t)steps * m32 * af * 512;
+    const size_t ah = (size_t)steps * m32 * 2 * 512;
     std::vector<float> scale(co), rs(co);
     for (int m = 0; m < co; ++m) {
       float mx = 0.f;
@@ -245,10 +244,9 @@ struct ExtdmHandle {
                     const float v = w[((size_t)m * ci + c) * kk + ky * ks + kx] * scale[m];
                     const _Float16 hi = (_Float16)v;
                     const _Float16 lo = (_Float16)(v - (float)hi);
-                    const size_t base = (((((size_t)mtile * ncgb + cb) * ks + ky) * steps + g * ks + kx) * m32 + q) * af;
+                    const size_t base = (((((size_t)mtile * ncgb + cb) * ks + ky) * steps + g * ks + kx) * m32 + q) * 2;
                     a[(base + 0) * 512 + l * 8 + e] = hi;
                     a[(base + 1) * 512 + l * 8 + e] = lo;
-                    if (af == 3) a[(base + 2) * 512 + l * 8 + e] = (_Float16)((float)hi * (1.f / X3_LO_UP));
                   }
     pw.wx = dmalloc(a.size() * sizeof(_Float16));
     HIPCHK(hipMemcpy(pw.wx, a.data(), a.size() * sizeof(_Float16), hipMemcpyHostToDevice));

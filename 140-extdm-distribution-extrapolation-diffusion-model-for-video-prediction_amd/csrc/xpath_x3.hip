@@ -33,32 +33,11 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 constexpr int KSTEPS = 3 * 13;  // (ci, dy); 16 dx columns per step
 
 __device__ __forceinline__ f32x16 mma3(const h8& ah, const h8& al, const h8& bh, const h8& bl, f32x16 c) {
+  // the scaled-lo product last, so its lo_dn VALU is off the head of the chain
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(lo_dn(ah), bl, c, 0, 0, 0);  // scaled x lo (gather8)
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(lo_dn(ah), bl, c, 0, 0, 0);  // scaled x lo (gather8p)
   return c;
-}
-
-// hi / lo fragments of 8 consecutive columns xs .. xs+7 of row y of an L x L plane, zero
-// outside the plane and for columns e >= ncol. The loads are unconditional (clamped
-// addresses, masked values): exec-masked per-element loads serialised this gather.
-__device__ __forceinline__ void gather8(const float* plane, int y, int xs, int L, int ncol, bool ok, h8& bh, h8& bl,
-                                        int& bad) {
-  const bool rowok = ok && y >= 0 && y < L;
-  const int yc = y < 0 ? 0 : (y >= L ? L - 1 : y);
-  const float* row = plane + (long)yc * L;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int xx = xs + e;
-    const int xc = xx < 0 ? 0 : (xx >= L ? L - 1 : xx);
-    // opaque before the mask, so the load cannot be sunk into a per-element branch
-    const float ld = split_src(row[xc]);
-    const float v = (rowok && e < ncol && xx >= 0 && xx < L) ? ld : 0.f;
-    bad |= fabsf(v) >= 65504.f;
-    const _Float16 hi = (_Float16)v;
-    bh[e] = hi;
-    bl[e] = (_Float16)((v - (float)hi) * X3_LO_UP);  // scaled lo (split2s, kernels.h)
-  }
 }
 
 // hi / lo' fragments of 8 consecutive values of a row of the zero-padded copy of x (xpad_kernel):

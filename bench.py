@@ -228,27 +228,32 @@ class NativeWorkload:
                        'rounds': self.rounds, 'parallelism': f'clip-shard x{self.world} (+all-gather)',
                        'workspace_gb': round(self.h.workspace_bytes() / 2 ** 30, 2)}}
 
-    # extdm_bench_layer ids (runtime.cpp) of the kernels reported, dominant first: the
-    # level-0 ResnetBlock 3x3 conv (64 -> 64 at the latent size; block1's conv stages an fp32
-    # input, block2's copies block1's pre-split operand, id 5), init_conv's cond_fea branch
-    # (256 -> 64, 7x7), the level-0 1x1 res_conv (128 -> 64, HBM-bound: 3 FLOP-equivalents
-    # of f16x3 MFMA per 4-B element moved is far below the machine balance), and the
-    # attention launches: level-0 shifted-window attention (6), the temporal attention (7)
-    # and TrajWarp's cross-attention core (8). `kernel`: the launched template; the PMC
-    # traffic of profiles/pmc_layer<id>.json counts only when it names this template and
-    # was measured on this exact library build (lib_sha16).
-    LAYERS = [(1, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0>',
+    # extdm_bench_layer ids (runtime.cpp) of the kernels reported, dominant first: the kernel
+    # with the largest share of a step's GPU time, init_conv's cond_fea branch (256 -> 64,
+    # 7x7, one ~4 ms launch per step: 15 % of the DDIM-20 profile's kernel time,
+    # profiles/r03_b64_ddim20_kernel_stats.csv), then the level-0 ResnetBlock 3x3 conv (64 ->
+    # 64 at the latent size; block1's conv stages an fp32 input, block2's copies block1's
+    # pre-split operand, id 5), the level-0 1x1 res_conv (128 -> 64, HBM-bound: 3
+    # FLOP-equivalents of f16x3 MFMA per 4-B element moved is far below the machine balance),
+    # the attention launches: level-0 shifted-window attention (6), the temporal attention (7)
+    # and TrajWarp's cross-attention core (8), and the x-branch's low-K gathers (9, 10).
+    # `kernel`: the launched template; the PMC traffic of profiles/pmc_layer<id>.json counts
+    # only when it names this template and was measured on this exact library build
+    # (lib_sha16).
+    LAYERS = [(0, 'mfma', 'conv_x3_kernel<7, 1, 64, 512, 1, 8, 16, 1, true, 1, false, false, 0>',
+               'init_conv cond_fea branch 256->64 1x7x7'),
+              (1, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0>',
                'level-0 ResnetBlock block1 conv 64->64 1x3x3, fp32 input staged'),
               (6, 'mfma', 'attn_x3_kernel<64, 0, 32, 8, true>',
                'level-0 shifted-window attention (STW, C 64, 2x4x4 windows, 8 heads x 32), fused LN/qkv/proj'),
               (5, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true, false, 0>',
                'level-0 ResnetBlock block2 conv 64->64 1x3x3, pre-split operand by LDS-DMA'),
-              (0, 'mfma', 'conv_x3_kernel<7, 1, 64, 512, 1, 8, 16, 1, true, 1, false, false, 0>',
-               'init_conv cond_fea branch 256->64 1x7x7'),
               (7, 'mfma', 'attn_x3_kernel<64, 1, 32, 8, false>', 'init_temporal_attn (C 64, 16 frames, 8 heads x 32)'),
               (8, 'mfma', 'cross_attn_x3p_kernel', 'TrajWarp cross-attention core (3584 queries x 512 keys, 8 heads)'),
               (4, 'hbm', 'conv_x3_kernel<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, false, 0>',
-               'level-0 res_conv 128->64 1x1x1')]
+               'level-0 res_conv 128->64 1x1x1'),
+              (9, 'mfma', 'xpath_x3_kernel<2>', 'init_conv x-branch as one composed 13x13 conv 3->64, K = 3x169'),
+              (10, 'mfma', 'noise_pool_x3_kernel', 'init_noise_conv 3->256 1x7x7 + MaxPool(1,2,2), K = 3x49')]
 
     def _traffic(self, layer, kname):
         """HBM bytes per launch from the committed PMC passes (scripts_gpu/pmc_layers.sh), only
