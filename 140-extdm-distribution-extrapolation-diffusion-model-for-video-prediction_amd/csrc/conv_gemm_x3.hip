@@ -79,7 +79,10 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
   const int wm = wave / WAVES_N;
   const int wn = wave % WAVES_N;
   const int h = lane >> 5, lc = lane & 31;
-  const long n0 = (long)blockIdx.x * BN;
+  // XCD-aware column-tile order (conv_x3.hip tile note): XCD k takes a contiguous range of
+  // column tiles, so the input rows neighbouring tiles both gather come from its L2
+  const long nb = (gridDim.x & 7) ? (long)blockIdx.x : (long)((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3));
+  const long n0 = nb * BN;
   const int mt = blockIdx.y;
   const int par = blockIdx.z;  // deconv parity (py, px)
   const int py = par >> 1, px = par & 1;

@@ -252,9 +252,12 @@ __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __rest
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lc = lane & 31, h = lane >> 5;
   const int nqb = (NQ + 127) / 128;
-  const int qb = blockIdx.x % nqb;
-  const int hd = (blockIdx.x / nqb) % heads;
-  const int b = blockIdx.x / (nqb * heads);
+  // XCD-aware block order (conv_x3.hip tile note): the query blocks of one (b, head) on one
+  // XCD, so its pre-split K / V come from that XCD's L2
+  const int bid = (gridDim.x & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3));
+  const int qb = bid % nqb;
+  const int hd = (bid / nqb) % heads;
+  const int b = bid / (nqb * heads);
   const int qi = qb * 128 + wave * 32 + lc;
   const bool qvalid = qi < NQ;
   const float* qp = Q + ((long)b * C + hd * 32) * NQ;

@@ -48,16 +48,17 @@ __device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned&
 // The weight side's product is exact while a_hi * 2^-11 is normal (|a_hi| >= 2^-3 in the
 // row-scaled units, whose row maximum is 2^14..2^15); the few smaller weights lose bits only
 // in a term 2^-17 below the row's largest. Same LDS-only rule as split2.
+// 4 VALU per pair: V = 2^11 (a, b) as one v_pk_mul_f32 (exact), then lo' = fp16(-hi 2^11 + V)
+// by v_fma_mix{lo,hi}_f16 reading hi from the packed register (the fma is exact, one rounding:
+// the bits of fp16((v - hi) 2^11))
+typedef float f32x2s_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split2s(float a, float b, unsigned& hi, unsigned& lo) {
-  float da, db;
-  asm("v_cvt_pk_f16_f32 %0, %4, %5\n\t"
-      "v_fma_mix_f32 %2, -%0, 1.0, %4 op_sel_hi:[1,0,0]\n\t"
-      "v_fma_mix_f32 %3, -%0, 1.0, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]\n\t"
-      "v_ldexp_f32 %2, %2, 11\n\t"
-      "v_ldexp_f32 %3, %3, 11\n\t"
-      "v_cvt_pk_f16_f32 %1, %2, %3"
-      : "=&v"(hi), "=v"(lo), "=&v"(da), "=&v"(db)
-      : "v"(a), "v"(b));
+  const f32x2s_t V = (f32x2s_t){a, b} * 2048.f;
+  asm("v_cvt_pk_f16_f32 %0, %2, %3\n\t"
+      "v_fma_mixlo_f16 %1, -%0, %6, %4 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %1, -%0, %6, %5 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(hi), "=&v"(lo)
+      : "v"(a), "v"(b), "v"(V.x), "v"(V.y), "s"(2048.f));
 }
 constexpr float X3_LO_UP = 2048.f;
 // the weight-side factor of the scaled-lo product (exact power of two, 4 v_pk_mul_f16 per h8)

@@ -259,10 +259,38 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   // Layout [c][r = td*4 + th][32], the 16-B chunk q of row r stored at q ^ r: the 32 lanes of
   // a half-wave (8 rows x 4 columns of one channel) read 32 distinct banks ((a/4) mod 32 for
   // 4-B accesses; shifted windows straddle two chunks at complementary column offsets).
-  static_assert(!TILE || (MODE == 0 && C == 64 && NW == 8), "tile path: level-0 STW only");
+  static_assert(!TILE || (C == 64 && NW == 8), "tile path: C = 64, 8 waves");
+  // T0: the MODE 0 tile above. T1: MODE 1 (temporal, 16 frames, two pixels per wave): the
+  // workgroup's 16 consecutive pixels x 16 frames x C, as [c][16-B chunk q][frame t][4 px]
+  // (one 1-KiB LDS-DMA instruction per channel: lane l = (q = l >> 4, t = l & 15) loads the
+  // 16 B of pixels 4q .. 4q+3 of frame t), so the prologue reads x from LDS (2-way bank
+  // conflicts: frames t and t + 8 share banks), the residual comes from the tile and the
+  // output leaves as 16-B row pieces; gamma and the inner LayerNorm's w / b are in LDS too.
+  // The per-lane path spent 31.7K of ~112K cycles per wave in the prologue (strided x loads and
+  // per-element parameter loads) and 23.4K in the epilogue (s_memtime stamps, B = 64).
+  constexpr bool T0 = TILE && MODE == 0, T1 = TILE && MODE == 1;
   float* const tileT = reinterpret_cast<float*>(wsm + 2 * UL::HALVES);
+  // behind the tile: T0 gamma + proj bias, T1 gamma + LayerNorm w + b (192 floats)
+  float* const parL = tileT + C * 256;
+  const int hw0 = T1 ? ((wg * NW) % groups_per_sample) * 2 : 0;  // T1: the workgroup's first pixel
+  if (T1) {
+#pragma unroll
+    for (int i = 0; i < C / NW; ++i) {
+      const int c = wave + i * NW;
+      __builtin_amdgcn_global_load_lds((const void*)(xb + (long)c * sc + (lane & 15) * st + hw0 + 4 * (lane >> 4)),
+                                       (lds_ptr_t)(tileT + c * 256), 16, 0, 0);
+    }
+    if (wave == 0 && lane < 48)
+      __builtin_amdgcn_global_load_lds((const void*)(lane < 16 ? gamma + 4 * lane
+                                                     : (lane < 32 ? ln_w + 4 * (lane - 16) : ln_b + 4 * (lane - 32))),
+                                       (lds_ptr_t)parL, 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // T1: this lane's (frame, pixel) in the tile
+  const int t1idx = ((2 * wave + (lc >> 4)) >> 2) * 64 + (lc & 15) * 4 + ((2 * wave + (lc >> 4)) & 3);
   int trow[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // element offset of tile row r in a channel plane
-  if (TILE) {
+  if (T0) {
     const int grp0 = (wg * NW) % groups_per_sample;
     const int nWw = g.Wp / g.ws2, nWh = g.Hp / g.ws1;
     const int wh = (grp0 / nWw) % nWh, wd = grp0 / (nWw * nWh);
@@ -294,7 +322,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   // window class of the bias / mask table (MODE 0 shifted layers): bit d for the last
   // window along a shifted dim d
   int pat = 0;
-  if (TILE && npat > 1) {
+  if (T0 && npat > 1) {
     // the workgroup's row of windows: ww = wave, (wd, wh) of its first window
     const int grp0 = (wg * NW) % groups_per_sample;
     const int nWd = g.Dp / g.ws0, nWh = g.Hp / g.ws1;
@@ -311,7 +339,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 
   // ---- 1. normalisation into register fragments ----
   Tok me;
-  if (TILE) {  // every token of a tile window exists and lies inside the volume
+  if (T0) {  // every token of a tile window exists and lies inside the volume
     me.pos = 0; me.valid = 1; me.exists = 1; me.lab = 0; me.rpos = lc;
   } else {
     me = token_of<MODE>(lc, g, st, grp);
@@ -322,7 +350,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   h8 xh[KS], xl[KS];
   float m1 = 0.f, den1 = 1.f, rden1 = 1.f, gi = 1.f;
   // e_w reduction slots (NW floats) behind everything else the kernel keeps in LDS
-  float* const redL = reinterpret_cast<float*>(wsm + 2 * UL::HALVES) + (TILE || PIPE ? C * 256 + 128 + 2048 : 0);
+  float* const redL = reinterpret_cast<float*>(wsm + 2 * UL::HALVES) + (TILE || PIPE ? C * 256 + 192 + 2048 : 0);
   {
     float xv[KS][8];
     float s = 0.f;
@@ -330,8 +358,8 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     for (int k = 0; k < KS; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        xv[k][e] = TILE ? tileT[(16 * k + 8 * h + e) * 256 + tidx]
-                                  : ldb(rs_x, vpro, (int)((16 * k + e) * sc * 4));
+        xv[k][e] = T0 ? tileT[(16 * k + 8 * h + e) * 256 + tidx]
+                   : T1 ? tileT[(16 * k + 8 * h + e) * 256 + t1idx] : ldb(rs_x, vpro, (int)((16 * k + e) * sc * 4));
         s += xv[k][e];
       }
     s = xh_sum(s);
@@ -357,14 +385,14 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       for (int k = 0; k < KS; ++k)
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          xv[k][e] = (xv[k][e] - m1) * rv * (TILE ? tileT[C * 256 + 16 * k + 8 * h + e] : ldb(rs_g, 32 * h, (16 * k + e) * 4));
+          xv[k][e] = (xv[k][e] - m1) * rv * (T0 ? parL[16 * k + 8 * h + e] : ldb(rs_g, 32 * h, (16 * k + e) * 4));
     } else {
       float s2 = 0.f;
 #pragma unroll
       for (int k = 0; k < KS; ++k)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          xv[k][e] = (xv[k][e] - m1) * rden1 * ldb(rs_g, 32 * h, (16 * k + e) * 4);
+          xv[k][e] = (xv[k][e] - m1) * rden1 * (T1 ? parL[16 * k + 8 * h + e] : ldb(rs_g, 32 * h, (16 * k + e) * 4));
           s2 += xv[k][e];
         }
       s2 = xh_sum(s2);
@@ -380,8 +408,8 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       for (int k = 0; k < KS; ++k)
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          xv[k][e] = ((xv[k][e] - m2) * rstd2 * ldb(rs_lw, 32 * h, (16 * k + e) * 4) +
-                      ldb(rs_lb, 32 * h, (16 * k + e) * 4)) * vm;
+          xv[k][e] = ((xv[k][e] - m2) * rstd2 * (T1 ? parL[64 + 16 * k + 8 * h + e] : ldb(rs_lw, 32 * h, (16 * k + e) * 4)) +
+                      (T1 ? parL[128 + 16 * k + 8 * h + e] : ldb(rs_lb, 32 * h, (16 * k + e) * 4))) * vm;
     }
     // e_w: the workgroup's largest |normalised value| to [2^8, 2^9) (a LayerNorm whose variance
     // is below its eps leaves the output far from unit scale, so this is data-dependent);
@@ -446,7 +474,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   // tile path: the factors (the same in every wave: token = lane) go to LDS as [8 float4][64
   // lanes] and are re-read per unit (8 conflict-free ds_read_b128) instead of holding 32
   // VGPRs through the unit loop
-  float4* const ropeL = reinterpret_cast<float4*>(tileT + C * 256 + 128);
+  float4* const ropeL = reinterpret_cast<float4*>(tileT + C * 256 + 192);
   if ((TILE || PIPE) && wave == 0) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -649,7 +677,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       f32x16 bia[HPU];
       if (j >= 1) load_bias(j - 1, bia);
       if (j + 1 <= UNITS) load_step(j + 1, wsm + ((j + 1) & 1) * UL::HALVES);
-      if (TILE && j == UNITS) {
+      if (T0 && j == UNITS) {
         // the x tile again for the residual epilogue, into the fragments' place (no wave reads
         // them after step UNITS - 1): in flight during the last unit's attention
         const int r = lane >> 3, qq = (lane & 7) ^ r;
@@ -725,9 +753,32 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   // 16 frame planes per instruction, 8 bytes each, and every 64-B line is written by 8
   // waves. Instead the workgroup's 16 consecutive pixels x D frames x C channels go through
   // LDS ([c][t][16 px], rows padded for conflict-free lane writes) and leave as 64-B rows.
-  const bool lds_epi = MODE == 1 && C == 64 && NW == 8 && g.D <= 16 && groups_per_sample % NW == 0 && (g.H * g.W) % 16 == 0 &&
-                       (osc & 3) == 0 && (st & 3) == 0 && (((uintptr_t)out) & 15) == 0;
-  if (MODE == 1 && lds_epi) {
+  const bool lds_epi = !T1 && MODE == 1 && C == 64 && NW == 8 && g.D <= 16 && groups_per_sample % NW == 0 &&
+                       (g.H * g.W) % 16 == 0 && (osc & 3) == 0 && (st & 3) == 0 && (((uintptr_t)out) & 15) == 0;
+  if (T1) {
+    // residual from the tile, the result back into it (each (channel, frame, pixel) is one
+    // lane's), then the tile leaves as 16-B pieces (the DMA's mapping in reverse)
+    const float spj = wsc[3];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ch = ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float* tp = tileT + ch * 256 + t1idx;
+        const float xv = *tp;
+        *tp = pacc[ct][r] * spj + (xv + (xv - m1) * rden1 * parL[ch]);
+      }
+    __syncthreads();
+    float* o0 = ob + hw0;
+#pragma unroll
+    for (int i = 0; i < C * 64 / (NW * 64); ++i) {
+      const int id = tid + i * NW * 64;
+      const int c = id >> 6, l = id & 63;
+      const float4 v = *reinterpret_cast<const float4*>(tileT + c * 256 + 4 * l);
+      *reinterpret_cast<float4*>(o0 + (long)c * osc + (long)(l & 15) * st + 4 * (l >> 4)) = v;
+    }
+    stamp(19);
+  } else if (MODE == 1 && lds_epi) {
     constexpr int RS = 20, CS = 16 * RS + 8;  // CS % 16 == 8: the two lane halves hit other banks
     float* T = reinterpret_cast<float*>(wsm);
     __syncthreads();  // every wave is done with the weight ring
@@ -757,6 +808,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
         *reinterpret_cast<float4*>(o0 + (long)c * osc + (long)t * st + 4 * q) = v;
       }
     }
+    stamp(19);
   } else if (active && me.valid) {
     if (dbg & 8) {  // timing only: no epilogue loads / stores (one store keeps the work live)
       float acc = 0.f;
@@ -777,9 +829,9 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
         for (int r = 0; r < 16; ++r) {
           const int cu = ct * 32 + (r & 3) + 8 * (r >> 2);
           // MODE 0: proj bias; MODE 1: gamma
-          const float pb = TILE ? tileT[C * 256 + 64 + cu + 4 * h] : ldb(rs_b, 16 * h, cu * 4);
+          const float pb = T0 ? parL[64 + cu + 4 * h] : ldb(rs_b, 16 * h, cu * 4);
           const float y = pacc[ct][r] * spj;
-          if (TILE) {
+          if (T0) {
             // residual from the tile, the result back into it (each (channel, token) is one lane's)
             float* tp = tileT + (cu + 4 * h) * 256 + tidx;
             *tp = (y + pb) + *tp;
@@ -795,7 +847,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     }
     stamp(19);
   }
-  if (TILE) {
+  if (T0) {
     // the tile leaves as whole 128-B lines: chunk id -> (channel, row, stored chunk), its
     // global chunk undoes the row's swizzle
     __syncthreads();
@@ -810,6 +862,15 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       *reinterpret_cast<float4*>(ob + (long)c * osc + roff + 4 * (qs ^ r)) = v;
     }
   }
+}
+
+// The MODE 1 tile path (kernel, T1): 16 frames, whole workgroups of 16 pixels inside a sample,
+// 16-B aligned rows; x and out share their channel / frame strides (temporal_x3).
+bool attn_x3_tile1_ok(const View& x, const View& out, const AttnGeom& g, int groups) {
+  static const bool off = [] { const char* v = getenv("EXTDM_X3_NO_TILE"); return v && v[0] && v[0] != '0'; }();
+  return !off && g.mode == 1 && g.D == 16 && (g.H * g.W) % 16 == 0 && groups % 8 == 0 && x.st == (long)x.H * x.W &&
+         x.st % 4 == 0 && x.sc % 4 == 0 && x.sb % 4 == 0 && out.sc % 4 == 0 && out.sb % 4 == 0 && out.st == x.st &&
+         ((uintptr_t)x.p & 15) == 0 && ((uintptr_t)out.p & 15) == 0;
 }
 
 // The MODE 0 tile path (kernel header, "tile path"): 2x4x4 windows over W = 32 without
@@ -830,14 +891,14 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
   // MODE 1 at C = 64, 8 waves: the epilogue's [C][16 frames][16 px] staging tile (rows of
   // 20, channels of 328 floats) reuses the ring
   const size_t ring = (size_t)2 * UnitLayout<C>::HALVES * sizeof(_Float16);
-  const bool tile = MODE == 0 && C == 64 && NW == 8 && attn_x3_tile_ok(x, out, g, groups);
+  const bool tile = C == 64 && NW == 8 &&
+                    (MODE == 0 ? attn_x3_tile_ok(x, out, g, groups) : attn_x3_tile1_ok(x, out, g, groups));
   size_t lds = (MODE == 1 && C == 64 && NW == 8) ? std::max(ring, (size_t)C * 328 * sizeof(float)) : ring;
-  // tile / PIPE (C = 64): behind the ring the x tile or the normalised fragments (C * 256
-  // floats), gamma + proj bias (128), the RoPE factors (8 x 64 float4)
-  if (tile || C == 64) lds = std::max(lds, ring + ((size_t)C * 8 * 32 + 2 * 64 + 8 * 64 * 4) * sizeof(float));
-  // + the e_w reduction slots (MODE 1's epilogue staging may overlap them: dead by then)
-  lds = std::max(lds, ring + (size_t)((tile || C == 64) ? C * 8 * 32 + 2 * 64 + 8 * 64 * 4 : 0) * sizeof(float) +
-                          NW * sizeof(float));
+  // tile / C = 64: behind the ring the x tile (C * 256 floats), 192 floats of norm / bias
+  // parameters, the RoPE factors (8 x 64 float4), then the e_w reduction slots (MODE 1's
+  // non-tile epilogue staging may overlap them: dead by then)
+  const size_t behind = (tile || C == 64) ? (size_t)C * 8 * 32 + 192 + 8 * 64 * 4 : 0;
+  lds = std::max(lds, ring + (behind + NW) * sizeof(float));
   // per device, once: the dynamic-LDS limit
   static std::once_flag once[64];
   int dev = 0;
@@ -845,8 +906,8 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
   std::call_once(once[dev & 63], [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW, false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (MODE == 0 && C == 64 && NW == 8)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW, MODE == 0 && C == 64 && NW == 8>),
+    if (C == 64 && NW == 8)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW, C == 64 && NW == 8>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
   const int total = x.B * groups;
@@ -856,7 +917,7 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
     (void)hipMalloc(&ts, (size_t)total * 24 * sizeof(long long));
     (void)hipMemsetAsync(ts, 0, (size_t)total * 24 * sizeof(long long), s);
   }
-  constexpr bool TILE_OK = MODE == 0 && C == 64 && NW == 8;
+  constexpr bool TILE_OK = C == 64 && NW == 8;
   auto kern = tile ? &attn_x3_kernel<C, MODE, DH, NW, TILE_OK> : &attn_x3_kernel<C, MODE, DH, NW, false>;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, s, x.p, out.p, x.sb, x.sc, x.st, out.sb, out.sc, g, gamma,
                      lw, lb, reinterpret_cast<const _Float16*>(wpk), wsc, bp, mbias, npat, rcos, rsin, q_scale, groups,

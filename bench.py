@@ -248,7 +248,7 @@ class NativeWorkload:
                'level-0 shifted-window attention (STW, C 64, 2x4x4 windows, 8 heads x 32), fused LN/qkv/proj'),
               (5, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true, false, 0>',
                'level-0 ResnetBlock block2 conv 64->64 1x3x3, pre-split operand by LDS-DMA'),
-              (7, 'mfma', 'attn_x3_kernel<64, 1, 32, 8, false>', 'init_temporal_attn (C 64, 16 frames, 8 heads x 32)'),
+              (7, 'mfma', 'attn_x3_kernel<64, 1, 32, 8, true>', 'init_temporal_attn (C 64, 16 frames, 8 heads x 32), x tile by LDS-DMA'),
               (8, 'mfma', 'cross_attn_x3p_kernel', 'TrajWarp cross-attention core (3584 queries x 512 keys, 8 heads)'),
               (4, 'hbm', 'conv_x3_kernel<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, false, 0>',
                'level-0 res_conv 128->64 1x1x1'),
