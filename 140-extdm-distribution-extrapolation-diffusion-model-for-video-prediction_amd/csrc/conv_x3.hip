@@ -698,10 +698,9 @@ void launch(hipStream_t s, const X3Args& a, unsigned ntiles) {
 
 X3Tile x3_tile(int ks, int cout) {
   X3Tile t{};
-  // 7x7 (init_conv): 16 waves over 64 x 512 px tiles, one X buffer; 3x3: 8 waves
+  // 7x7 (init_conv): 8 waves over 64 x 512 px tiles, one X buffer; 3x3: 8 waves
   if (ks == 7) {
-    // EXTDM_X3_BN7=256: the 8-wave 64 x 256 tile (two X buffers, no spills) instead of the
-    // 16-wave 64 x 512 one (148 B of scratch per lane outside the MFMA loop)
+    // EXTDM_X3_BN7=256: the 8-wave 64 x 256 tile (two X buffers) instead of 64 x 512
     static const int bn7 = [] { const char* v = getenv("EXTDM_X3_BN7"); return v ? atoi(v) : 512; }();
     t.bm = 64; t.bn = bn7 == 256 ? 256 : 512; t.ng = 1;
   }
@@ -795,7 +794,12 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     return true;
   }
   if (tl.bn == 512) {
-    if (ks == 7 && tl.bm == 64) launch<7, 1, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
+    // 7x7 64 x 512 tile: 8 waves of 64 x 64 (two per SIMD, 256 registers, no scratch):
+    // 4.02 -> 3.80 ms at B = 64 against 16 waves of 32 x 64 (128 registers, 132-148 B of
+    // scratch per lane); EXTDM_X3_NW7=16 restores the 16-wave tile (A/B)
+    static const int nw7 = [] { const char* v = getenv("EXTDM_X3_NW7"); return v ? atoi(v) : 8; }();
+    if (ks == 7 && tl.bm == 64 && nw7 != 16) launch<7, 1, 64, 512, 1, 8, 8, 1>(s, a, ntiles);
+    else if (ks == 7 && tl.bm == 64) launch<7, 1, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
     else if (ks == 3 && tl.bm == 64) launch<3, 1, 64, 512, 1, 8, 16, 1>(s, a, ntiles);
     else return false;
     return true;

@@ -240,7 +240,7 @@ class NativeWorkload:
     # `kernel`: the launched template; the PMC traffic of profiles/pmc_layer<id>.json counts
     # only when it names this template and was measured on this exact library build
     # (lib_sha16).
-    LAYERS = [(0, 'mfma', 'conv_x3_kernel<7, 1, 64, 512, 1, 8, 16, 1, true, 1, false, false, 0>',
+    LAYERS = [(0, 'mfma', 'conv_x3_kernel<7, 1, 64, 512, 1, 8, 8, 1, true, 2, false, false, 0>',
                'init_conv cond_fea branch 256->64 1x7x7'),
               (1, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0>',
                'level-0 ResnetBlock block1 conv 64->64 1x3x3, fp32 input staged'),
