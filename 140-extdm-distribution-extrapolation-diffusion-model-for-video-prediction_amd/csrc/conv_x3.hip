@@ -686,6 +686,28 @@ int x3_v3() {
   return v3;
 }
 
+// 3x3 128 x 128 tile on 4 waves of 64 x 64 (12 MFMAs per 8 ds_read_b128, two workgroups per
+// CU) when its LDS fits half a CU; else 8 waves of 32 x 64 at one workgroup per CU.
+// EXTDM_X3_W128=8 keeps the 8-wave tile everywhere (A/B).
+bool x3_w128_4(const X3Args& a, bool xop) {
+  static const int w = [] { const char* v = getenv("EXTDM_X3_W128"); return v ? atoi(v) : 4; }();
+  if (w == 8) return false;
+  constexpr size_t AH = 3 * 4 * 2 * 512;
+  const size_t xlo = xop ? (size_t)((a.XPOS + 63) & ~63) * 16 : (size_t)a.XPOS * 16;
+  return (2 * AH + 2 * 2 * xlo + 32 + 4 * 128) * sizeof(_Float16) <= 80 * 1024;
+}
+// split-K thresholds of the 3x3 128-row tile (launch_wg, total_wg): 8 waves at one workgroup
+// per CU split below 128 workgroups, up to 256; the 4-wave tile (two per CU) below
+// EXTDM_X3_SPLIT4 = "wg,total" (default 256,512)
+void x3_split128(bool four, long& max_wg, long& max_total) {
+  static const long* t4 = [] {
+    static long v[2] = {256, 512};
+    if (const char* e = getenv("EXTDM_X3_SPLIT4")) sscanf(e, "%ld,%ld", &v[0], &v[1]);
+    return v;
+  }();
+  if (four) { max_wg = t4[0]; max_total = t4[1]; } else { max_wg = 128; max_total = 256; }
+}
+
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF>
 void launch(hipStream_t s, const X3Args& a, unsigned ntiles) {
   // EXTDM_X3_NOSPAN=1: per-stage __syncthreads() (A/B against the spanning barriers)
@@ -814,9 +836,17 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     else launch<3, 1, 64, 256, 1, 4, 4, 2>(s, a, ntiles);
   }
   else if (ks == 3 && tl.bm == 128) {
-    if (split_k(a, ntiles, epi, 128, 256)) {
+    const bool four = x3_w128_4(a, false);
+    long mw, mt;
+    x3_split128(four, mw, mt);
+    if (four && split_k(a, ntiles, epi, mw, mt)) {
+      launch_sp<3, 1, 128, 128, 1, 2, 4, 2, true, 1, false, false, 1>(s, a, ntiles);
+      launch_sp<3, 1, 128, 128, 1, 2, 4, 2, true, 1, false, false, 2>(s, a, ntiles);
+    } else if (!four && split_k(a, ntiles, epi, mw, mt)) {
       launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, false, false, 1>(s, a, ntiles);
       launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, false, false, 2>(s, a, ntiles);
+    } else if (four) {
+      launch<3, 1, 128, 128, 1, 2, 4, 2>(s, a, ntiles);
     } else {
       launch<3, 1, 128, 128, 1, 2, 8, 2>(s, a, ntiles);
     }
@@ -851,7 +881,11 @@ size_t conv_x3_split_bytes(const View& out, const View& in0, const View* in1, co
   unsigned ntiles = 0;
   if (w.mode != MODE_CONV || w.KH != w.KW || !x3_setup(out, in0, in1, w, ConvEpi{}, a, ntiles, nullptr)) return 0;
   if (w.xbn == 512 || w.xbm != 128) return 0;
-  if (w.KH == 3) return split_bytes(a, ntiles, split_slices(a, ntiles, 128, 256));
+  if (w.KH == 3) {
+    long mw, mt;
+    x3_split128(x3_w128_4(a, false), mw, mt);
+    return split_bytes(a, ntiles, split_slices(a, ntiles, mw, mt));
+  }
   if (w.KH == 1) return split_bytes(a, ntiles, split_slices(a, ntiles, 384, 512));
   return 0;
 }
@@ -862,7 +896,9 @@ size_t conv_x3_op_split_bytes(const View& out, const PackedW& w, int C) {
   unsigned ntiles = 0;
   const View g = cf_view(nullptr, out.B, C, out.T, out.H, out.W);
   if (!x3_setup(out, g, nullptr, w, ConvEpi{}, a, ntiles, nullptr)) return 0;
-  return split_bytes(a, ntiles, split_slices(a, ntiles, 128, 256));
+  long mw, mt;
+  x3_split128(x3_w128_4(a, true), mw, mt);
+  return split_bytes(a, ntiles, split_slices(a, ntiles, mw, mt));
 }
 
 size_t x3op_halves(int B, int C, int T, int H, int W, int pad) {
@@ -906,9 +942,19 @@ bool conv_x3_forward_op(hipStream_t s, const View& out, const X3Op& in, const Pa
   if (w.xbm == 64) {
     if (x3_v3() == 1) launch_sp<3, 3, 64, 256, 1, 4, 8, 2, true, 1, true>(s, a, ntiles);
     else launch_sp<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true>(s, a, ntiles);
-  } else if (split_k(a, ntiles, epi, 128, 256)) {
+    return true;
+  }
+  const bool four = x3_w128_4(a, true);
+  long mw, mt;
+  x3_split128(four, mw, mt);
+  if (four && split_k(a, ntiles, epi, mw, mt)) {
+    launch_sp<3, 1, 128, 128, 1, 2, 4, 2, true, 1, true, false, 1>(s, a, ntiles);
+    launch_sp<3, 1, 128, 128, 1, 2, 4, 2, true, 1, true, false, 2>(s, a, ntiles);
+  } else if (!four && split_k(a, ntiles, epi, mw, mt)) {
     launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true, false, 1>(s, a, ntiles);
     launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true, false, 2>(s, a, ntiles);
+  } else if (four) {
+    launch_sp<3, 1, 128, 128, 1, 2, 4, 2, true, 1, true>(s, a, ntiles);
   } else {
     launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true>(s, a, ntiles);
   }
