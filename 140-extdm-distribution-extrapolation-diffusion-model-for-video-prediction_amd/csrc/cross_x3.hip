@@ -245,106 +245,151 @@ __device__ __forceinline__ void split2s(float a, float b, h8& hi, h8& lo, int e)
   lo[e] = pl.x; lo[e + 1] = pl.y;
 }
 
+// Per 32-key tile the VALU is the bound (MFMA 14 x 32 cycles against ~260 vector
+// instructions per tile in the first form), so the loop carries only what the tile needs:
+//  - the K lo x Q lo scores term rides in the cross-term accumulator (Q's unscaled lo as
+//    a third fragment, qd): one fma combines a score instead of two;
+//  - 1/sqrt(dk) and log2 e folded into Q: scores come out in log2 units;
+//  - lazy rescaling: the running maximum a lane's probabilities are taken against moves
+//    only when a new score exceeds it by more than 2^8 in probability (any lane of the
+//    wave: one wave-uniform branch), so P <= 2^8 -- exact in the hi / scaled-lo split
+//    -- and the 32 accumulator multiplies and the alpha exp are off the common path;
+//  - the key mask only in a partial tail tile (wave-uniform branch);
+//  - two tiles per loop trip over two fragment sets (no register rotation copies).
+// A wave owns QS sets of 32 queries: each K / V fragment read from L2 serves QS sets
+// (QS = 2 halves the L2 fragment traffic: 7.5 GB per B = 64 launch at QS = 1).
+template <int QS>
 __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __restrict__ Q,
                                                              const _Float16* __restrict__ kvp, float* __restrict__ O,
                                                              int C, int heads, int NQ, int NK, int nkt,
                                                              int* __restrict__ range) {
+  constexpr float LOG2E = 1.44269504088896341f;
+  constexpr float TAU = 8.f;  // log2 of the largest probability before a rescale
+  constexpr int QB = 128 * QS;  // queries per block
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lc = lane & 31, h = lane >> 5;
-  const int nqb = (NQ + 127) / 128;
+  const int nqb = (NQ + QB - 1) / QB;
   // XCD-aware block order (conv_x3.hip tile note): the query blocks of one (b, head) on one
   // XCD, so its pre-split K / V come from that XCD's L2
   const int bid = (gridDim.x & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3));
   const int qb = bid % nqb;
   const int hd = (bid / nqb) % heads;
   const int b = bid / (nqb * heads);
-  const int qi = qb * 128 + wave * 32 + lc;
-  const bool qvalid = qi < NQ;
   const float* qp = Q + ((long)b * C + hd * 32) * NQ;
   int bad = 0;
-  h8 qh[2], ql[2];
+  // qh = fp16(v), ql = fp16((v - hi) 2^11), qd = fp16(v - hi) (the lo x lo term's operand)
+  h8 qh[QS][2], ql[QS][2], qd[QS][2];
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int u = 0; u < QS; ++u) {
+    const int qi = qb * QB + (wave * QS + u) * 32 + lc;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float v = qvalid ? qp[(long)(16 * s + 8 * h + e) * NQ + qi] * 0.17677669529663687f : 0.f;
-      bad |= fabsf(v) >= 65504.f;
-      SPLIT_S(v, qh[s][e], ql[s][e]);
-    }
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v =
+            qi < NQ ? qp[(long)(16 * s + 8 * h + e) * NQ + qi] * (0.17677669529663687f * LOG2E) : 0.f;
+        bad |= fabsf(v) >= 65504.f;
+        const float v_ = split_src(v);
+        const _Float16 a_ = (_Float16)v_;
+        qh[u][s][e] = a_;
+        ql[u][s][e] = (_Float16)((v_ - (float)a_) * LO_UP);
+        qd[u][s][e] = (_Float16)(v_ - (float)a_);
+      }
+  }
   const _Float16* base = kvp + ((long)b * heads + hd) * nkt * 8 * 512 + lane * 8;
   // fragments of a tile: [k | v][s][hl], 1 KiB apart
-  h8 f[8], fn[8];
+  h8 f0[8], f1[8];
   auto load = [&](int kt, h8* dst) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) dst[i] = *reinterpret_cast<const h8*>(base + ((long)kt * 8 + i) * 512);
   };
-  f32x16 oh, ox;
+  f32x16 oh[QS], ox[QS];
+  float mk[QS], l[QS];  // mk: the reference maximum, log2 units
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { oh[r] = 0.f; ox[r] = 0.f; }
-  float m = -INFINITY, l = 0.f;
-  load(0, f);
-  for (int kt = 0; kt < nkt; ++kt) {
-    if (kt + 1 < nkt) load(kt + 1, fn);
-    const int j0 = 32 * kt;
-    f32x16 sh, sx, sxx;
+  for (int u = 0; u < QS; ++u) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { sh[r] = 0.f; sx[r] = 0.f; sxx[r] = 0.f; }
+    for (int r = 0; r < 16; ++r) { oh[u][r] = 0.f; ox[u][r] = 0.f; }
+    mk[u] = -INFINITY;
+    l[u] = 0.f;
+  }
+  auto tile = [&](int kt, const h8* f) __attribute__((always_inline)) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const h8 ah = f[2 * s], al = f[2 * s + 1];
-      sh = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[s], sh, 0, 0, 0);
-      sx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh[s], sx, 0, 0, 0);
-      sx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql[s], sx, 0, 0, 0);
-      sxx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ql[s], sxx, 0, 0, 0);
-    }
-    float cm = -INFINITY;
-    const bool full = j0 + 32 <= NK;  // wave-uniform: no key mask in a full tile
+    for (int u = 0; u < QS; ++u) {
+      f32x16 sh, sx;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int j = j0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float sc = fmaf(fmaf(sxx[r], LO_DN, sx[r]), LO_DN, sh[r]);
-      const float sv = (full || j < NK) ? sc : -INFINITY;
-      sh[r] = sv;
-      cm = fmaxf(cm, sv);
-    }
-    cm = fmaxf(cm, __shfl_xor(cm, 32));
-    const float mn = fmaxf(m, cm);
-    if (mn != -INFINITY) {  // a fully padded tail tile (never the first) adds nothing
-      const float mnl = mn * 1.44269504088896341f;
-      const float alpha = __builtin_amdgcn_exp2f(fmaf(m, 1.44269504088896341f, -mnl));
+      for (int r = 0; r < 16; ++r) { sh[r] = 0.f; sx[r] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const h8 ah = f[2 * s], al = f[2 * s + 1];
+        sh = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[u][s], sh, 0, 0, 0);
+        sx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh[u][s], sx, 0, 0, 0);
+        sx = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql[u][s], sx, 0, 0, 0);
+        sx = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qd[u][s], sx, 0, 0, 0);
+      }
+      float cm = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sh[r] = fmaf(sx[r], LO_DN, sh[r]);
+        cm = fmaxf(cm, sh[r]);
+      }
+      const int j0 = 32 * kt;
+      if (j0 + 32 > NK) {  // partial tail tile (wave-uniform)
+        cm = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int j = j0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          sh[r] = j < NK ? sh[r] : -INFINITY;
+          cm = fmaxf(cm, sh[r]);
+        }
+      }
+      cm = fmaxf(cm, __shfl_xor(cm, 32));
+      if (__any(cm > mk[u] + TAU)) {  // rare after the first tile
+        const float mn = fmaxf(mk[u], cm);
+        const float alpha = __builtin_amdgcn_exp2f(mk[u] - mn);  // 0 on the first tile
+        l[u] *= alpha;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { oh[u][r] *= alpha; ox[u][r] *= alpha; }
+        mk[u] = mn;
+      }
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        sh[r] = __builtin_amdgcn_exp2f(fmaf(sh[r], 1.44269504088896341f, -mnl));
+        sh[r] = __builtin_amdgcn_exp2f(sh[r] - mk[u]);
         ps += sh[r];
       }
-      ps += __shfl_xor(ps, 32);
-      l = l * alpha + ps;
-      m = mn;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { oh[r] *= alpha; ox[r] *= alpha; }
+      l[u] += ps + __shfl_xor(ps, 32);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         h8 ph, pl;
 #pragma unroll
         for (int e = 0; e < 8; e += 2) split2s(sh[8 * s2 + e], sh[8 * s2 + e + 1], ph, pl, e);
         const h8 vh = f[4 + 2 * s2], vl = f[5 + 2 * s2];
-        oh = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, oh, 0, 0, 0);
-        ox = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, ox, 0, 0, 0);
-        ox = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, ox, 0, 0, 0);
+        oh[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, oh[u], 0, 0, 0);
+        ox[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, ox[u], 0, 0, 0);
+        ox[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, ox[u], 0, 0, 0);
       }
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) f[i] = fn[i];
+  };
+  load(0, f0);
+  for (int kt = 0; kt < nkt; kt += 2) {
+    if (kt + 1 < nkt) load(kt + 1, f1);
+    tile(kt, f0);
+    if (kt + 1 >= nkt) break;
+    if (kt + 2 < nkt) load(kt + 2, f0);
+    tile(kt + 1, f1);
   }
   if (bad) atomicOr(range, 1);
-  if (qvalid) {
-    float* ob = O + ((long)b * C + hd * 32) * NQ + qi;
-    const float il = 1.f / l;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int dd = (r & 3) + 8 * (r >> 2) + 4 * h;
-      ob[(long)dd * NQ] = (oh[r] + ox[r] * LO_DN) * il;
+  for (int u = 0; u < QS; ++u) {
+    const int qi = qb * QB + (wave * QS + u) * 32 + lc;
+    if (qi < NQ) {
+      float* ob = O + ((long)b * C + hd * 32) * NQ + qi;
+      const float il = 1.f / l[u];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int dd = (r & 3) + 8 * (r >> 2) + 4 * h;
+        ob[(long)dd * NQ] = (oh[u][r] + ox[u][r] * LO_DN) * il;
+      }
     }
   }
 }
@@ -367,9 +412,13 @@ bool cross_kv_split(hipStream_t s, const float* k, const float* v, _Float16* kvp
 bool cross_attention_x3p(hipStream_t s, const float* q, const _Float16* kvp, float* o, int B, int C, int heads, int NQ,
                          int NK) {
   if (C != 32 * heads || NK < 1 || NQ < 1) return false;
-  const unsigned nblocks = (unsigned)(B * heads * ((NQ + 127) / 128));
-  hipLaunchKernelGGL(cross_attn_x3p_kernel, dim3(nblocks), dim3(256), 0, s, q, kvp, o, C, heads, NQ, NK,
-                     (NK + 31) / 32, x3_range_ptr());
+  // QS = 1: QS = 2 needs 256 VGPRs (one wave per SIMD) and measured 0.63 -> 0.94 ms at
+  // B = 64; EXTDM_CROSS_QS=2 selects it (A/B)
+  static const int qs_env = [] { const char* e = getenv("EXTDM_CROSS_QS"); return e ? atoi(e) : 0; }();
+  const int qs = qs_env == 2 ? 2 : 1;
+  const unsigned nblocks = (unsigned)(B * heads * ((NQ + 128 * qs - 1) / (128 * qs)));
+  hipLaunchKernelGGL(qs == 2 ? cross_attn_x3p_kernel<2> : cross_attn_x3p_kernel<1>, dim3(nblocks), dim3(256), 0, s,
+                     q, kvp, o, C, heads, NQ, NK, (NK + 31) / 32, x3_range_ptr());
   return true;
 }
 

@@ -249,7 +249,7 @@ class NativeWorkload:
               (5, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true, false, 0>',
                'level-0 ResnetBlock block2 conv 64->64 1x3x3, pre-split operand by LDS-DMA'),
               (7, 'mfma', 'attn_x3_kernel<64, 1, 32, 8, true>', 'init_temporal_attn (C 64, 16 frames, 8 heads x 32), x tile by LDS-DMA'),
-              (8, 'mfma', 'cross_attn_x3p_kernel', 'TrajWarp cross-attention core (3584 queries x 512 keys, 8 heads)'),
+              (8, 'mfma', 'cross_attn_x3p_kernel<1>', 'TrajWarp cross-attention core (3584 queries x 512 keys, 8 heads)'),
               (4, 'hbm', 'conv_x3_kernel<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, false, 0>',
                'level-0 res_conv 128->64 1x1x1'),
               (9, 'mfma', 'xpath_x3_kernel<2>', 'init_conv x-branch as one composed 13x13 conv 3->64, K = 3x169'),
