@@ -251,20 +251,36 @@ __device__ __forceinline__ void split2s(float a, float b, h8& hi, h8& lo, int e)
 //    a third fragment, qd): one fma combines a score instead of two;
 //  - 1/sqrt(dk) and log2 e folded into Q: scores come out in log2 units;
 //  - lazy rescaling: the running maximum a lane's probabilities are taken against moves
-//    only when a new score exceeds it by more than 2^8 in probability (any lane of the
-//    wave: one wave-uniform branch), so P <= 2^8 -- exact in the hi / scaled-lo split
-//    -- and the 32 accumulator multiplies and the alpha exp are off the common path;
+//    only when a new score exceeds it by more than 2^4 in probability (any lane of the
+//    wave: one wave-uniform branch), so the 48 accumulator multiplies and the alpha exp
+//    are off the common path; P <= 2^4 is taken as P' = 2^11 P (<= 2^15, in the exp2
+//    argument), whose lo half fp16(P' - hi') needs no scaling multiply (split2u): V's
+//    scaled lo x P' hi then sits at 2^22 in its own accumulator (ox2);
 //  - the key mask only in a partial tail tile (wave-uniform branch);
 //  - two tiles per loop trip over two fragment sets (no register rotation copies).
 // A wave owns QS sets of 32 queries: each K / V fragment read from L2 serves QS sets
 // (QS = 2 halves the L2 fragment traffic: 7.5 GB per B = 64 launch at QS = 1).
+// unscaled split of a pair of probabilities already scaled by 2^11 (P' = 2^11 P <= 2^15):
+// hi' = fp16 pair = 2^11 fp16(P) in the normal range, lo' = fp16(P' - hi') (the difference
+// exact in fp32): the scaled-lo pair without its multiply
+__device__ __forceinline__ void split2u(float a, float b, h8& hi, h8& lo, int e) {
+  const float a_ = split_src(a), b_ = split_src(b);
+  const f16x2_t ph = __builtin_convertvector((f32x2_t){a_, b_}, f16x2_t);
+  const float one = split_src(1.0f);
+  const float la = __builtin_fmaf(-(float)ph.x, one, a_);
+  const float lb = __builtin_fmaf(-(float)ph.y, one, b_);
+  const f16x2_t pl = __builtin_convertvector((f32x2_t){la, lb}, f16x2_t);
+  hi[e] = ph.x; hi[e + 1] = ph.y;
+  lo[e] = pl.x; lo[e + 1] = pl.y;
+}
+
 template <int QS>
 __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __restrict__ Q,
                                                              const _Float16* __restrict__ kvp, float* __restrict__ O,
                                                              int C, int heads, int NQ, int NK, int nkt,
                                                              int* __restrict__ range) {
   constexpr float LOG2E = 1.44269504088896341f;
-  constexpr float TAU = 8.f;  // log2 of the largest probability before a rescale
+  constexpr float TAU = 4.f;  // log2 of the largest probability before a rescale (P' <= 2^15)
   constexpr int QB = 128 * QS;  // queries per block
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lc = lane & 31, h = lane >> 5;
@@ -303,12 +319,13 @@ __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __rest
 #pragma unroll
     for (int i = 0; i < 8; ++i) dst[i] = *reinterpret_cast<const h8*>(base + ((long)kt * 8 + i) * 512);
   };
-  f32x16 oh[QS], ox[QS];
-  float mk[QS], l[QS];  // mk: the reference maximum, log2 units
+  // O' = 2^11 O as oh (V hi x P' hi) + ox (V hi x P' lo) + 2^-11 ox2 (V scaled lo x P' hi)
+  f32x16 oh[QS], ox[QS], ox2[QS];
+  float mk[QS], l[QS];  // mk: the reference maximum, log2 units; l = sum of P'
 #pragma unroll
   for (int u = 0; u < QS; ++u) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { oh[u][r] = 0.f; ox[u][r] = 0.f; }
+    for (int r = 0; r < 16; ++r) { oh[u][r] = 0.f; ox[u][r] = 0.f; ox2[u][r] = 0.f; }
     mk[u] = -INFINITY;
     l[u] = 0.f;
   }
@@ -348,13 +365,14 @@ __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __rest
         const float alpha = __builtin_amdgcn_exp2f(mk[u] - mn);  // 0 on the first tile
         l[u] *= alpha;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { oh[u][r] *= alpha; ox[u][r] *= alpha; }
+        for (int r = 0; r < 16; ++r) { oh[u][r] *= alpha; ox[u][r] *= alpha; ox2[u][r] *= alpha; }
         mk[u] = mn;
       }
       float ps = 0.f;
+      const float mkb = mk[u] - 11.f;  // P' = 2^11 P
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        sh[r] = __builtin_amdgcn_exp2f(sh[r] - mk[u]);
+        sh[r] = __builtin_amdgcn_exp2f(sh[r] - mkb);
         ps += sh[r];
       }
       l[u] += ps + __shfl_xor(ps, 32);
@@ -362,22 +380,27 @@ __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __rest
       for (int s2 = 0; s2 < 2; ++s2) {
         h8 ph, pl;
 #pragma unroll
-        for (int e = 0; e < 8; e += 2) split2s(sh[8 * s2 + e], sh[8 * s2 + e + 1], ph, pl, e);
+        for (int e = 0; e < 8; e += 2) split2u(sh[8 * s2 + e], sh[8 * s2 + e + 1], ph, pl, e);
         const h8 vh = f[4 + 2 * s2], vl = f[5 + 2 * s2];
         oh[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, oh[u], 0, 0, 0);
-        ox[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, ox[u], 0, 0, 0);
+        ox2[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, ox2[u], 0, 0, 0);
         ox[u] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, ox[u], 0, 0, 0);
       }
     }
   };
+  // two tiles per trip over the two fragment sets, the odd tail after the loop: no exit in
+  // the middle of a trip (that form kept the O accumulators in different registers on the
+  // two paths: a loop-carried copy of all 48 per trip); the last trip's set-0 load re-reads
+  // the final tile instead of branching around it
   load(0, f0);
-  for (int kt = 0; kt < nkt; kt += 2) {
-    if (kt + 1 < nkt) load(kt + 1, f1);
+  int kt = 0;
+  for (; kt + 1 < nkt; kt += 2) {
+    load(kt + 1, f1);
     tile(kt, f0);
-    if (kt + 1 >= nkt) break;
-    if (kt + 2 < nkt) load(kt + 2, f0);
+    load(min(kt + 2, nkt - 1), f0);
     tile(kt + 1, f1);
   }
+  if (kt < nkt) tile(kt, f0);
   if (bad) atomicOr(range, 1);
 #pragma unroll
   for (int u = 0; u < QS; ++u) {
@@ -388,7 +411,7 @@ __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __rest
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int dd = (r & 3) + 8 * (r >> 2) + 4 * h;
-        ob[(long)dd * NQ] = (oh[u][r] + ox[u][r] * LO_DN) * il;
+        ob[(long)dd * NQ] = fmaf(ox2[u][r], LO_DN, oh[u][r] + ox[u][r]) * il;
       }
     }
   }
