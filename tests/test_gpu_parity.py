@@ -108,6 +108,25 @@ def test_unet_forward_vs_oracle_other_t():
     assert (eps - ref).abs().max().item() <= 1e-4
 
 
+@pytest.mark.parametrize('tc,latent,fs', [(3, 8, 4), (2, 24, 12), (3, 24, 12)])
+def test_trajwarp_key_tiles_vs_oracle(tc, latent, fs):
+    """TrajWarp cross-attention (u12:804-827) over key counts the BAIR shapes never reach:
+    NK = tc * fs^2 = 48 (one full 32-key tile + a partial one), 288 (an odd count of full
+    tiles: the tail after the two-tile loop) and 432 (13 full + a partial tail), through
+    the whole u12 forward against the oracle."""
+    cfg = pkg.spec.UnetConfig(dim=16, tc=tc, tp=4, latent=latent, fea_size=fs)
+    x, t, cond, fea = unet_inputs(cfg, B=2, seed=5)
+    h = pkg._lib.Handle(cfg, 1000, 2, 0)
+    sd = make_sd(cfg)
+    sd.update(pkg.schedule_buffers(1000))
+    h.load_state(sd)
+    h.finalize()
+    eps = gpu_eps(h, x, t, cond, fea)
+    with torch.no_grad():
+        ref = oracle().unet_forward(make_sd(cfg), cfg.as_dict(), x, t, cond, fea)
+    assert (eps - ref).abs().max().item() <= 1e-4
+
+
 def test_batch_independence_bitwise():
     """Per-sample results do not depend on batch composition (sharding-safe)."""
     cfg = CONFIGS['small']
