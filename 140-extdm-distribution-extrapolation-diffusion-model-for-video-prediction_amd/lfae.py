@@ -351,6 +351,40 @@ class FlowDiffusion(nn.Module):
         return self.decode(ret, pred, ref)
 
 
+class _WrapperFlowDiffusion(FlowDiffusion):
+    """FlowDiffusion with the wrapper fixed by the class, as the reference fixes it by the
+    module its FlowDiffusion is imported from (scripts/DM/valid.py imports
+    model.BaseDM_adaptor.<DM_arch>.FlowDiffusion)."""
+    WRAPPER = 'multi_w_ref'
+
+    def __init__(self, *args, **kwargs):
+        kwargs.setdefault('wrapper', self.WRAPPER)
+        if kwargs['wrapper'] != self.WRAPPER:
+            raise ValueError(f'{type(self).__name__} mirrors the {self.WRAPPER} wrapper, not {kwargs["wrapper"]}')
+        super().__init__(*args, **kwargs)
+
+
+class FlowDiffusionMultiWRef(_WrapperFlowDiffusion):
+    """VideoFlowDiffusion_multi_w_ref.FlowDiffusion (:18-316)."""
+    WRAPPER = 'multi_w_ref'
+
+
+class FlowDiffusionMultiWRefU22(_WrapperFlowDiffusion):
+    """VideoFlowDiffusion_multi_w_ref_u22.FlowDiffusion (:143-510)."""
+    WRAPPER = 'multi_w_ref_u22'
+
+
+class FlowDiffusionMulti1248(_WrapperFlowDiffusion):
+    """VideoFlowDiffusion_multi1248.FlowDiffusion (:213-295)."""
+    WRAPPER = 'multi1248'
+
+
+# reference module name (config `DM_arch`, valid.py's import) -> FlowDiffusion class
+FLOW_DIFFUSION_BY_MODULE = {'VideoFlowDiffusion_multi_w_ref': FlowDiffusionMultiWRef,
+                            'VideoFlowDiffusion_multi_w_ref_u22': FlowDiffusionMultiWRefU22,
+                            'VideoFlowDiffusion_multi1248': FlowDiffusionMulti1248}
+
+
 @torch.no_grad()
 def autoregressive_sample(model, real_vids, total_pred_frames, num_sample_video=1, cond_scale=1.0, seed=None,
                           sample_base=0, round_noise=None):

@@ -9,7 +9,8 @@ import pytest
 from tests.golden_inputs import PKG
 
 yaml = pytest.importorskip('yaml')
-configs = importlib.import_module(PKG + '.configs')
+configs = importlib.import_module(PKG + ".configs")
+pkg = importlib.import_module(PKG)
 REF = '/root/reference/config/DM'
 
 pytestmark = pytest.mark.skipif(not os.path.isdir(REF), reason='reference configs absent')
@@ -39,3 +40,18 @@ def test_load_dm_config_reads_reference_yaml(name):
     assert cfg['flow_params']['model_params']['generator_params']['pixelwise_flow_predictor_params'][
         'estimate_occlusion_map'] is False
     assert cfg['dataset_params']['frame_shape'] == configs.dm_config(name)['dataset_params']['frame_shape']
+
+
+def test_flow_diffusion_by_module_fixes_the_wrapper():
+    """valid.py picks the sampling wrapper by importing FlowDiffusion from the module
+    named by DM_arch; FLOW_DIFFUSION_BY_MODULE is the same switch as a class lookup."""
+    cfg = pkg.configs.dm_config('bair')
+    want = {'VideoFlowDiffusion_multi_w_ref': 'multi_w_ref',
+            'VideoFlowDiffusion_multi_w_ref_u22': 'multi_w_ref_u22',
+            'VideoFlowDiffusion_multi1248': 'multi1248'}
+    assert set(pkg.FLOW_DIFFUSION_BY_MODULE) == set(want)
+    for mod, cls in pkg.FLOW_DIFFUSION_BY_MODULE.items():
+        fd = cls(config=cfg, is_train=False)
+        assert isinstance(fd, pkg.FlowDiffusion) and fd.wrapper == want[mod]
+    with pytest.raises(ValueError):
+        pkg.FlowDiffusionMultiWRef(config=cfg, is_train=False, wrapper='multi1248')
