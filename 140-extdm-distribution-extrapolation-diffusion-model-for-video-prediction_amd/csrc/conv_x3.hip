@@ -51,6 +51,9 @@ struct X3Args {
   const _Float16* xop; long xop_cg, xop_hl;  // halves per channel group / per hi|lo half
   // split-K (SPL): fp32 partial accumulators [z][mtile][tile][TM*TN*16][NT], nsplit slices
   float* part; int nsplit;
+  // PH: F's four edge lines [P][4 (top, bottom, left, right)][W][Cin] (fp32), written by the
+  // m-tile-0 workgroups while staging (fea_x3.hip reads them); null: not written
+  float* edge;
   ConvEpi e;
 };
 
@@ -85,6 +88,8 @@ template <> struct XMaxX3<3, 128> { static constexpr int v = 288; };
 template <> struct XMaxX3<1, 128> { static constexpr int v = 128; };
 template <> struct XMaxX3<7, 512> { static constexpr int v = 836; };
 template <> struct XMaxX3<3, 512> { static constexpr int v = 800; };
+template <> struct XMaxX3<5, 512> { static constexpr int v = 800; };
+template <> struct XMaxX3<5, 256> { static constexpr int v = 400; };
 
 // Stage barriers. SPAN = false: __syncthreads() per (channel block, ky) stage. While an
 // A-slot LDS-DMA is in flight its fence waits vmcnt(0), which also drains the X prefetch
@@ -110,9 +115,12 @@ template <> struct XMaxX3<3, 512> { static constexpr int v = 800; };
 // by the per-stage weight stream of too few CUs): 1 = slice blockIdx.z of the channel
 // blocks, accumulators stored as fp32 partials; 2 = the partials summed in slice order
 // (deterministic) and the normal epilogue.
+// PH: phase output (the composed fea conv, conv_x3_phase_forward): m-tile = output phase
+// (py, px) of a x2 upsampled map, row m - mtile * BM = output channel, tile pixel (row, col)
+// stored at (2 row + py, 2 col + px) of the 2H x 2W output.
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
-          bool RGN = false, int SPL = 0>
-__global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
+          bool RGN = false, int SPL = 0, bool PH = false>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 && KS == 5 ? 2 : 1))) void conv_x3_kernel(X3Args a) {
   constexpr int NT = NW * 64;
   constexpr int PAD = KS / 2;
   constexpr int CIB = 16 * NG;
@@ -383,11 +391,41 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
   // more = false, so that hipcc sees the X prefetch and its store_x in one region with no
   // X load pending across a loop back edge (a path-insensitive pending load there made it
   // wait vmcnt(0) before re-loading the xr registers, right behind the stage's A DMA).
+  // PH: F's edge lines from the staged tile of channel block cgb (m-tile 0 only): each edge
+  // position's 16 channels as hi + lo' 2^-11 (exactly the operand the MFMAs use; the edge
+  // kernels' own split of it gives back the same hi / lo'), into a.edge [P][4][W][Cin]. Issued
+  // before the stage's A DMA, so the stage barrier's counted wait retires these stores too.
+  auto export_edges = [&](const _Float16* Xs, int cgb) __attribute__((always_inline)) {
+    const int nrec = a.NP * 4 * a.W;
+    for (int r = tid; r < nrec; r += NT) {
+      const int pp = r / (4 * a.W), rem = r - pp * 4 * a.W, line = rem / a.W, jj = rem - line * a.W;
+      const int q = plane0 + pp;
+      const int iy = line == 0 ? 0 : (line == 1 ? a.H - 1 : jj);
+      const int ix = line == 2 ? 0 : (line == 3 ? a.W - 1 : jj);
+      if (q >= a.P || iy < row0 || iy >= row0 + a.TH) continue;
+      const int pos = (pp * THK + iy - row0 + PAD) * a.RS + ix + PAD;
+      const int sw = (pos >> 3) & 1;
+      const _Float16* xh = Xs + (long)pos * 16;
+      const h8 h0 = *reinterpret_cast<const h8*>(xh + 8 * sw), h1 = *reinterpret_cast<const h8*>(xh + 8 * (sw ^ 1));
+      const h8 l0 = *reinterpret_cast<const h8*>(xh + XLO + 8 * sw);
+      const h8 l1 = *reinterpret_cast<const h8*>(xh + XLO + 8 * (sw ^ 1));
+      float v[16];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        v[c] = (float)h0[c] + (float)l0[c] * (1.f / X3_LO_UP);
+        v[8 + c] = (float)h1[c] + (float)l1[c] * (1.f / X3_LO_UP);
+      }
+      float4* d = reinterpret_cast<float4*>(a.edge + (((long)q * 4 + line) * a.W + jj) * a.Cin + cgb * CIB);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) d[c] = make_float4(v[4 * c], v[4 * c + 1], v[4 * c + 2], v[4 * c + 3]);
+    }
+  };
   auto stage = [&](int cgb, int kb, bool more) __attribute__((always_inline)) {
     const int it = cgb * STG + kb;
     const int itr = it - c0 * STG, cr = cgb - c0;  // ring / buffer parity from the slice start
     const _Float16* Ast = (itr & 1) ? As1 : As0;
     const _Float16* Xs = (cr & 1) ? Xs1 : Xs0;
+    if (PH && !XOP && kb == 0 && a.edge && mtile == 0) export_edges(Xs, cgb);
     if (it + 1 < NIT) load_a(it + 1, (itr & 1) ? As0 : As1);
     const bool pre = (kb == 0) && more;
     if (SPAN) __builtin_amdgcn_sched_barrier(0);  // the X loads issue after the DMA (vmcnt order)
@@ -524,7 +562,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
       const bool valid = q0 < a.P && row0q < a.H;
       const int q = valid ? q0 : 0, row = valid ? row0q : 0;
       const int b = q / a.T, t = q - b * a.T;
-      const int pix = row * a.W + c;
+      const int pix = PH ? (2 * row + (mtile >> 1)) * (2 * a.W) + 2 * c + (mtile & 1) : row * a.W + c;
       float v[16];
 #pragma unroll
       for (int r16 = 0; r16 < 16; ++r16) v[r16] = acc[i][j][r16] * scl[r16] + bia[r16];
@@ -534,7 +572,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
 #pragma unroll
         for (int r16 = 0; r16 < 16; ++r16)
           rv[r16] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-              rs_res, (rbase + mrow[r16] * (int)a.e.res_sc) * 4, 0, 0));
+              rs_res, (rbase + (PH ? mrow[r16] - mtile * BM : mrow[r16]) * (int)a.e.res_sc) * 4, 0, 0));
         if (res_gn) {  // the arithmetic of gn_apply_plane_kernel (norm.hip), no FiLM
 #pragma unroll
           for (int r16 = 0; r16 < 16; ++r16) {
@@ -568,7 +606,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
       for (int r16 = 0; r16 < 16; ++r16) {
         const int m = mtile * BM + (wm * TM + i) * 32 + (r16 & 3) + 8 * (r16 >> 2) + 4 * h;
         const bool ok = valid && m < a.Cout;
-        const int off = ok ? (obase + m * (int)a.oc) * 4 : a.out_bytes;
+        const int off = ok ? (obase + (PH ? m - mtile * BM : m) * (int)a.oc) * 4 : a.out_bytes;
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r16]), rs_out, off, 0, 0);
         if (do_stats) {
           const float x = ok ? v[r16] : 0.f;
@@ -620,7 +658,7 @@ __global__ __launch_bounds__(NW * 64) void conv_x3_kernel(X3Args a) {
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
-          bool RGN = false, int SPL = 0>
+          bool RGN = false, int SPL = 0, bool PH = false>
 void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
   constexpr int AH = KY * NG * KS * (BM / 32) * 2 * 512;
   const size_t xlo = XOP ? (size_t)((a.XPOS + 63) & ~63) * 16 : (size_t)a.XPOS * NG * 16;
@@ -629,11 +667,11 @@ void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
   dim3 grid(ntiles, (a.Cout + BM - 1) / BM, SPL == 1 ? a.nsplit : 1);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL>), grid, dim3(NW * 64), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH>), grid, dim3(NW * 64), lds, s, a);
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN>
@@ -726,6 +764,10 @@ X3Tile x3_tile(int ks, int cout) {
     static const int bn7 = [] { const char* v = getenv("EXTDM_X3_BN7"); return v ? atoi(v) : 512; }();
     t.bm = 64; t.bn = bn7 == 256 ? 256 : 512; t.ng = 1;
   }
+  else if (ks == 5) {
+    // the phase-composed fea conv (conv_x3_phase_forward): one 64-row m-tile per output phase
+    t.bm = 64; t.bn = 512; t.ng = 1;
+  }
   else if (ks == 3) {
     // EXTDM_X3_BN3: pixel tile of the Cout <= 64 3x3 convs (256 or 512)
     static const int bn3 = [] { const char* v = getenv("EXTDM_X3_BN3"); return v ? atoi(v) : 256; }();
@@ -761,7 +803,8 @@ bool x3_setup(const View& out, const View& in0, const View* in1, const PackedW& 
   a.NP = tl.bn / (a.TH * W);
   a.RS = W + ks - 1;
   a.XPOS = a.NP * (a.TH + ks - 1) * a.RS;
-  const int xmax = tl.bn == 512 ? (ks == 7 ? 836 : 800) : (ks == 7 ? 560 : (ks == 3 ? (tl.bn == 256 ? 576 : 288) : 128));
+  const int xmax = tl.bn == 512 ? (ks == 7 ? 836 : 800)
+                                 : (ks == 7 ? 560 : (ks == 5 ? 400 : (ks == 3 ? (tl.bn == 256 ? 576 : 288) : 128)));
   if (a.XPOS > xmax) return false;
   a.in0 = in0.p; a.i0b = in0.sb; a.i0c = in0.sc; a.i0t = in0.st; a.C0 = in0.C;
   if (in1) { a.in1 = in1->p; a.i1b = in1->sb; a.i1c = in1->sc; a.i1t = in1->st; a.Cin = in0.C + in1->C; }
@@ -862,6 +905,44 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     }
   }
   else return false;
+  return true;
+}
+
+// The cond_fea half of init_conv over a bilinear x2 upsample of F, phase-composed
+// (runtime.cpp Pfea_phase): the 7x7 over the 2H x 2W upsampled map equals, per output phase
+// (py, px), a 5x5 over the zero-padded H x W map F plus edge corrections (fea_x3.hip). This
+// launch is the 5x5 part: Cout = 4 phases x C rows, out [B][C][T][2H][2W] (+= epi.res).
+// EXTDM_FEA_XBUF=1: one X buffer (A/B; default two).
+bool conv_x3_phase_forward(hipStream_t s, const View& out, const View& in, const PackedW& w, const ConvEpi& epi,
+                           float* edge) {
+  if (!w.wx || w.mode != MODE_CONV || w.KH != 5 || w.xbm != 64 || w.xbn != 512 || w.M != 4 * out.C) return false;
+  if (out.H != 2 * in.H || out.W != 2 * in.W || out.B != in.B || out.T != in.T || in.C * 25 != w.K) return false;
+  View og = out;  // the kernel's tile geometry: the input planes, 4C rows
+  og.H = in.H; og.W = in.W; og.C = w.M;
+  X3Args a;
+  unsigned ntiles = 0;
+  ConvEpi e = epi;
+  e.stats = nullptr;
+  // EXTDM_FEA_TILE=256: 64 x 256 px on 4 waves with one X buffer (66 KB of LDS: two workgroups
+  // per CU); default 64 x 512 on 8 waves
+  static const int bn = [] { const char* v = getenv("EXTDM_FEA_TILE"); return v ? atoi(v) : 512; }();
+  PackedW wt = w;
+  wt.xbn = bn == 256 ? 256 : 512;
+  if (!x3_setup(og, in, nullptr, wt, e, a, ntiles, nullptr)) return false;
+  auto extent = [&](long sb, long sc, long st) {
+    return ((long)(out.B - 1) * sb + (long)(out.C - 1) * sc + (long)(out.T - 1) * st + (long)out.H * out.W) * 4;
+  };
+  const long ob = extent(out.sb, out.sc, out.st);
+  const long rb = e.res ? extent(e.res_sb, e.res_sc, e.res_st) : 0;
+  if (ob >= (1L << 31) - 4 || rb >= (1L << 31) - 4) return false;
+  a.out_bytes = (int)ob;
+  a.res_bytes = (int)rb;
+  if (edge && (in.H != in.W || in.C % 16 != 0 || w.xng != 1)) return false;
+  a.edge = edge;
+  static const int xbuf = [] { const char* v = getenv("EXTDM_FEA_XBUF"); return v ? atoi(v) : 2; }();
+  if (wt.xbn == 256) launch_sp<5, 1, 64, 256, 1, 4, 4, 1, true, 2, false, false, 0, true>(s, a, ntiles);
+  else if (xbuf == 1) launch_sp<5, 1, 64, 512, 1, 8, 8, 1, true, 2, false, false, 0, true>(s, a, ntiles);
+  else launch_sp<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true>(s, a, ntiles);
   return true;
 }
 

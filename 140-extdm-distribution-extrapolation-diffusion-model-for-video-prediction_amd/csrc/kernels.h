@@ -200,6 +200,32 @@ size_t x3op_halves(int B, int C, int T, int H, int W, int pad);  // allocation i
 bool conv_x3_op_supported(const View& out, const PackedW& w, int C, int pad);
 bool conv_x3_forward_op(hipStream_t s, const View& out, const X3Op& in, const PackedW& w, const ConvEpi& epi,
                         int* stats_slots = nullptr);
+// init_conv's cond_fea branch over a bilinear x2 upsample of F [B][C][T][H][W], phase-composed
+// (fea_x3.hip header): the 5x5 part, out [B][Co][T][2H][2W] += (epi.res), weights [4 Co][C][5][5]
+// edge (non-null): F's four edge lines are written to edge [B*T][4][H][C] (fea_edge_floats)
+bool conv_x3_phase_forward(hipStream_t s, const View& out, const View& in, const PackedW& w, const ConvEpi& epi,
+                           float* edge = nullptr);
+// ... and its edge corrections from those lines, added into out (after the 5x5 launch):
+// side_w / side_scale the packed f16x3 line weights [pair][side][mtile][cb][tap][m32][hl][lane][8]
+// / row scales [pair][side][mt * 128], corner_w fp32 [corner][16 px][C][Co]
+struct FeaSideArgs {
+  const float* e;  // edge lines [P][4][L][C]
+  int C, L, T, P;
+  const _Float16* w; const float* wscale;
+  float* out; long ob, oc, ot; int OH, OW, Co;
+  int out_bytes, pair;
+  int* range;
+};
+struct FeaCornerArgs {
+  const float* e;
+  int C, L, T, P;
+  const float* dw;
+  float* out; long ob, oc, ot; int OH, OW, Co;
+};
+inline size_t fea_edge_floats(int P, int C, int L) { return (size_t)P * 4 * L * C; }
+bool fea_edges_supported(int C, int Co, int L);
+bool fea_edges_forward(hipStream_t s, const View& out, const float* edge, int C, const void* side_w,
+                       const float* side_scale, const float* corner_w);
 void x3_range_reset(hipStream_t s);
 // Evaluation metrics (metrics.hip): per-frame PSNR and SSIM in fp64.
 size_t frame_metrics_workspace(int nframes, int C, int H);

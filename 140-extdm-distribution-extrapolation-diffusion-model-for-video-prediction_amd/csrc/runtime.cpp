@@ -165,7 +165,7 @@ struct ExtdmHandle {
     pw.w = dmalloc(a.size() * sizeof(float));
     HIPCHK(hipMemcpy(pw.w, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
     if (kh == kw && (kh == 1 || kh == 3 || kh == 7) && co > 32) pack_halo(pw, t.f, ci);
-    if (x3_convs() && kh == kw && (kh == 1 || kh == 3 || kh == 7) && co > 32 &&
+    if (x3_convs() && kh == kw && (kh == 1 || kh == 3 || kh == 5 || kh == 7) && co > 32 &&
         ci >= 16)
       pack_x3(pw, t.f, ci);
     if (x3_convs()) pack_gemm_x3(pw, a, 1);
@@ -481,6 +481,164 @@ struct ExtdmHandle {
   }
   bool noise_pool_enabled() const {
     return xpath_enabled() && cfg.arch == EXTDM_ARCH_U12 && cfg.latent <= 32 && cfg.latent % 2 == 0;
+  }
+
+  // init_conv's cond_fea branch over F at fea_size instead of its bilinear x2 upsample
+  // (fea_x3.hip header, u12:1034-1041): the 5x5 phase kernels [4 Co][Cf][5][5] (packed by P as
+  // "init_conv.weight#fea5"), the f16x3 edge-line weights and the fp32 corner weights, composed
+  // in fp64. EXTDM_NO_FEA_PHASE=1: the bilinear launch and the 7x7 over the upsampled map (A/B).
+  struct FeaPhaseW { void* side = nullptr; float* side_scale = nullptr; float* corner = nullptr; };
+  FeaPhaseW fpw;
+  bool fea_phase_ready = false;
+  bool fea_phase_enabled() const {
+    static const bool off = [] { const char* v = getenv("EXTDM_NO_FEA_PHASE"); return v && v[0] && v[0] != '0'; }();
+    const int fs = cfg.fea_size;
+    return !off && xpath_enabled() && cfg.dim == 64 && cfg.latent == 2 * fs && (fs == 16 || fs == 32) &&
+           fea_edges_supported(cfg.fea_ch, cfg.dim, fs);
+  }
+  // up2 of a length-n axis, align_corners=False, as F.interpolate: weight of F[k] in row r
+  // (0 outside [0, 2n): the 7x7's zero padding), and the unclamped interpolation of the
+  // zero-padded F (any integer r)
+  static double up_true(int r, int k, int n) {
+    if (r < 0 || r >= 2 * n) return 0.0;
+    const double src = std::max(0.0, (r + 0.5) * 0.5 - 0.5);
+    const int k0 = (int)src, k1 = k0 < n - 1 ? k0 + 1 : k0;
+    const double lam = src - k0;
+    return (k == k0 ? 1.0 - lam : 0.0) + (k == k1 ? lam : 0.0);
+  }
+  static double up_inf(int r, int k) {
+    const int j = (r >= 0 ? r : r - 1) / 2;  // floor(r / 2)
+    if (k == j) return 0.75;
+    return (r - 2 * j == 0 ? k == j - 1 : k == j + 1) ? 0.25 : 0.0;
+  }
+  const FeaPhaseW& Pfea_phase() {
+    if (fea_phase_ready) return fpw;
+    Pxpath();  // the fea half of init_conv.weight
+    const HostTensor& wt = H("init_conv.weight#fea");  // [Co][Cf][1][7][7]
+    const int Co = (int)wt.shape[0], Cf = (int)wt.shape[1], n = cfg.fea_size;
+    REQUIRE(wt.shape.back() == 7 && Co == cfg.dim && Cf % 16 == 0, "phase-composed init_conv: unexpected weight");
+    auto W = [&](int co, int ci, int dy, int dx) { return (double)wt.f[(((size_t)co * Cf + ci) * 7 + dy) * 7 + dx]; };
+    // interior composition A[p][l][d]: weight of tap l (F[m - 2 + l]) in row 2m + p + d - 3 (any m)
+    double A[2][5][7];
+    for (int p = 0; p < 2; ++p)
+      for (int l = 0; l < 5; ++l)
+        for (int d = 0; d < 7; ++d) A[p][l][d] = up_inf(2 * 8 + p + d - 3, 8 - 2 + l);
+    // edge deltas: U - Uinf at column ke of output row r (nonzero for ke = 0 / n - 1 only)
+    auto delta = [&](int r, int ke) { return up_true(r, ke, n) - up_inf(r, ke); };
+    // main 5x5 phase kernels, row ph * Co + co, ph = 2 py + px
+    {
+      HostTensor k5;
+      k5.shape = {4 * (int64_t)Co, Cf, 1, 5, 5};
+      k5.f.assign((size_t)4 * Co * Cf * 25, 0.f);
+      std::vector<double> t(7 * 5);
+      for (int co = 0; co < Co; ++co)
+        for (int ci = 0; ci < Cf; ++ci)
+          for (int py = 0; py < 2; ++py)
+            for (int px = 0; px < 2; ++px) {
+              // t[dy][lx] = sum_dx W[dy][dx] A[px][lx][dx]
+              for (int dy = 0; dy < 7; ++dy)
+                for (int lx = 0; lx < 5; ++lx) {
+                  double s_ = 0.0;
+                  for (int dx = 0; dx < 7; ++dx) s_ += W(co, ci, dy, dx) * A[px][lx][dx];
+                  t[dy * 5 + lx] = s_;
+                }
+              for (int ly = 0; ly < 5; ++ly)
+                for (int lx = 0; lx < 5; ++lx) {
+                  double s_ = 0.0;
+                  for (int dy = 0; dy < 7; ++dy) s_ += A[py][ly][dy] * t[dy * 5 + lx];
+                  k5.f[((((size_t)(2 * py + px) * Co + co) * Cf + ci) * 5 + ly) * 5 + lx] = (float)s_;
+                }
+            }
+      host["init_conv.weight#fea5"] = std::move(k5);
+    }
+    // edge lines: [pair][side][row m = co * 8 + (d*2 + py)*2 + px][ci][tap], then f16x3-packed
+    const int R = 8 * Co, MT = (R + 127) / 128, RP = MT * 128, ncb = Cf / 16;
+    std::vector<double> ws((size_t)4 * R * Cf * 5, 0.0);
+    for (int pair = 0; pair < 2; ++pair)
+      for (int side = 0; side < 2; ++side) {
+        const int ke = side ? n - 1 : 0, base = side ? 2 * n - 4 : 0;
+        for (int d = 0; d < 2; ++d)
+          for (int py = 0; py < 2; ++py)
+            for (int px = 0; px < 2; ++px) {
+              // pair 0: output row y = base + 2d + py (the delta axis), columns by phase px;
+              // pair 1: output column x = base + 2d + px, rows by phase py
+              const int e = base + 2 * d + (pair ? px : py), ip = pair ? py : px;
+              double dl[7];
+              for (int k = 0; k < 7; ++k) dl[k] = delta(e + k - 3, ke);
+              for (int co = 0; co < Co; ++co) {
+                const int m = co * 8 + (d * 2 + py) * 2 + px;  // fea_x3.hip row order
+                for (int ci = 0; ci < Cf; ++ci)
+                  for (int l = 0; l < 5; ++l) {
+                    double s_ = 0.0;
+                    for (int dy = 0; dy < 7; ++dy)
+                      for (int dx = 0; dx < 7; ++dx)
+                        s_ += W(co, ci, dy, dx) * (pair ? dl[dx] * A[ip][l][dy] : dl[dy] * A[ip][l][dx]);
+                    ws[((((size_t)pair * 2 + side) * R + m) * Cf + ci) * 5 + l] = s_;
+                  }
+              }
+            }
+      }
+    const size_t ah = (size_t)5 * 4 * 2 * 512;  // halves per (mtile, cb): [tap][m32][hl][lane][8]
+    std::vector<_Float16> g((size_t)4 * MT * ncb * ah, (_Float16)0.f);
+    std::vector<float> rs((size_t)4 * RP, 1.f);
+    for (int ps = 0; ps < 4; ++ps)
+      for (int m = 0; m < R; ++m) {
+        double mx = 0.0;
+        for (size_t k = 0; k < (size_t)Cf * 5; ++k) mx = std::max(mx, std::fabs(ws[((size_t)ps * R + m) * Cf * 5 + k]));
+        int e2 = 0;
+        if (mx > 0.0) { std::frexp(mx, &e2); e2 = 15 - e2; }
+        rs[(size_t)ps * RP + m] = std::ldexp(1.f, -e2);
+        const int mtile = m / 128, m32 = (m % 128) / 32, lc = m % 32;
+        for (int ci = 0; ci < Cf; ++ci)
+          for (int l = 0; l < 5; ++l) {
+            const float v = (float)std::ldexp(ws[(((size_t)ps * R + m) * Cf + ci) * 5 + l], e2);
+            const int cb = ci / 16, lane = lc + 32 * ((ci % 16) / 8), e = ci % 8;
+            const size_t b0 = ((((size_t)ps * MT + mtile) * ncb + cb) * ah) + (size_t)((l * 4 + m32) * 2) * 512;
+            const _Float16 hi = (_Float16)v;
+            g[b0 + lane * 8 + e] = hi;
+            g[b0 + 512 + lane * 8 + e] = (_Float16)(v - (float)hi);
+          }
+      }
+    fpw.side = dmalloc(g.size() * sizeof(_Float16));
+    HIPCHK(hipMemcpy(fpw.side, g.data(), g.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    fpw.side_scale = dmalloc(rs.size() * sizeof(float));
+    HIPCHK(hipMemcpy(fpw.side_scale, rs.data(), rs.size() * sizeof(float), hipMemcpyHostToDevice));
+    // corners [corner = 2 (bottom) + (right)][p = yy * 4 + xx][ci][co]
+    std::vector<float> cw((size_t)4 * 16 * Cf * Co, 0.f);
+    for (int corner = 0; corner < 4; ++corner) {
+      const int ky = (corner >> 1) ? n - 1 : 0, kx = (corner & 1) ? n - 1 : 0;
+      const int yb = (corner >> 1) ? 2 * n - 4 : 0, xb = (corner & 1) ? 2 * n - 4 : 0;
+      for (int p = 0; p < 16; ++p) {
+        double dy_[7], dx_[7];
+        for (int k = 0; k < 7; ++k) {
+          dy_[k] = delta(yb + p / 4 + k - 3, ky);
+          dx_[k] = delta(xb + p % 4 + k - 3, kx);
+        }
+        for (int ci = 0; ci < Cf; ++ci)
+          for (int co = 0; co < Co; ++co) {
+            double s_ = 0.0;
+            for (int dy = 0; dy < 7; ++dy)
+              for (int dx = 0; dx < 7; ++dx) s_ += W(co, ci, dy, dx) * dy_[dy] * dx_[dx];
+            cw[(((size_t)corner * 16 + p) * Cf + ci) * Co + co] = (float)s_;
+          }
+      }
+    }
+    fpw.corner = dmalloc(cw.size() * sizeof(float));
+    HIPCHK(hipMemcpy(fpw.corner, cw.data(), cw.size() * sizeof(float), hipMemcpyHostToDevice));
+    fea_phase_ready = true;
+    return fpw;
+  }
+  // rp += init_conv's cond_fea branch of F [B][Cf][tp][fs][fs] (phase-composed)
+  void fea_phase_conv(const View& rp, const View& f) {
+    const FeaPhaseW& fw = Pfea_phase();
+    const PackedW& w5 = P("init_conv.weight#fea5");
+    Scope sc(arena);
+    float* edge = arena.alloc(fea_edge_floats(f.B * f.T, f.C, f.H));
+    if (plan) return;
+    ConvEpi e;
+    e.res = rp.p; e.res_sb = rp.sb; e.res_sc = rp.sc; e.res_st = rp.st;
+    REQUIRE(conv_x3_phase_forward(s, rp, f, w5, e, edge), "phase-composed init_conv launch rejected");
+    REQUIRE(fea_edges_forward(s, rp, edge, f.C, fw.side, fw.side_scale, fw.corner), "init_conv edge corrections rejected");
   }
 
   View alloc_cf(int B, int C, int T, int Hh, int Ww) {
@@ -1075,7 +1233,7 @@ struct ExtdmHandle {
   // TrajWarp passes fm = cond_fea[:, :, :tc] through unchanged, u12:792), TrajWarp's
   // k / v of fm, and for ada / ada_u22 the resized cond_adaptor + cond_temporal_attn
   // features (ada.py:1035-1036), which depend on cond_fea only.
-  View r_all, kv_k, kv_v, fup_all;
+  View r_all, kv_k, kv_v, fup_all, fa_all;  // fa_all: ada's adapted cond_fea at fea_size (phase path)
   _Float16* kvp = nullptr;  // k / v as pre-split MFMA fragments (cross_kv_split)
   void alloc_cond_cache() {
     const int Bm = cfg.max_batch, T = frames(), L = cfg.latent, fs = cfg.fea_size;
@@ -1089,6 +1247,8 @@ struct ExtdmHandle {
     }
     if (cfg.arch == EXTDM_ARCH_ADA || cfg.arch == EXTDM_ARCH_ADA_U22)
       fup_all = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * T * L * L * 4), Bm, cfg.fea_ch, T, L, L);
+    if (cfg.arch == EXTDM_ARCH_ADA && fea_phase_enabled())
+      fa_all = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * T * fs * fs * 4), Bm, cfg.fea_ch, T, fs, fs);
   }
   static View with_batch(View v, int B) { v.B = B; return v; }
 
@@ -1112,7 +1272,7 @@ struct ExtdmHandle {
       fup = alloc_cf(B, cfg.fea_ch, tc, L, L);
       if (!plan) bilinear_frames(s, fup, vf.frames(0, tc), vf.frames(0, tc), tc);
     } else {
-      View fa = alloc_cf(B, cfg.fea_ch, T, fs, fs);
+      View fa = fa_all.p ? with_batch(fa_all, B) : alloc_cf(B, cfg.fea_ch, T, fs, fs);
       if (!plan) copy_view(s, fa, vf);
       adaptor("cond_adaptor", fa);
       temporal("cond_temporal_attn", fa, fa);
@@ -1176,7 +1336,7 @@ struct ExtdmHandle {
           xpad = alloc_cf(B, 3, tp, xpad_size(L), xpad_size(L));
           if (!plan) xpad_forward(s, xpad, vx);
         }
-        View fu;
+        View fu, fpre;  // fpre: the cond_fea branch's input before its x2 upsample
         if (arch == EXTDM_ARCH_U12) {
           REQUIRE(L / 2 == fs, "TrajWarp: maxpooled latent must match cond_fea size");
           View xq = alloc_cf(B, 256, tp, fs, fs);
@@ -1190,16 +1350,21 @@ struct ExtdmHandle {
           }
           View fp2 = alloc_cf(B, cfg.fea_ch, tp, fs, fs);
           trajwarp_q(xq, vf, fp2);
-          fu = alloc_cf(B, cfg.fea_ch, tp, L, L);
-          if (!plan) bilinear_frames(s, fu, fp2, fp2, 0);
+          fpre = fp2;
+          if (!fea_phase_enabled()) {
+            fu = alloc_cf(B, cfg.fea_ch, tp, L, L);
+            if (!plan) bilinear_frames(s, fu, fp2, fp2, 0);
+          }
         } else {
           fu = with_batch(fup_all, B).frames(tc, tp);
+          if (fa_all.p) fpre = with_batch(fa_all, B).frames(tc, tp);
         }
         if (xp) {
-          // rp = K_class * x + cbias_class (x-branch + both biases), then rp += Wb * pad(fu)
+          // rp = K_class * x + cbias_class (x-branch + both biases), then rp += Wb * pad(up2(F))
           const XPathW& xw = Pxpath();
           if (!plan) REQUIRE(xpath_x3_forward(s, rp, xpad, xw.w, xw.rs, xw.cb), "composed init_conv launch rejected");
-          conv(rp, fu, nullptr, P("init_conv.weight#fea"), 1, 3, nullptr, &rp);
+          if (fea_phase_enabled()) fea_phase_conv(rp, fpre);  // over F itself (fea_x3.hip)
+          else conv(rp, fu, nullptr, P("init_conv.weight#fea"), 1, 3, nullptr, &rp);
         } else {
           conv(rp, x0p, &fu, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
         }
@@ -2151,6 +2316,44 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
       *flops_out = flop;
       return;
     }
+    // layers 0 / 11 with the phase-composed cond_fea branch (fea_x3.hip): 0 = the 5x5 phase conv
+    // over F (fea_size, 4 x dim rows, += into r as the forward issues it), 11 = its edge
+    // corrections (the two line launches and the corner launch)
+    if ((layer == 0 || layer == 11) && h->fea_phase_enabled()) {
+      const int fs = h->cfg.fea_size, Cf = h->cfg.fea_ch, Co = h->cfg.dim;
+      View f = h->alloc_cf(B, Cf, T, fs, fs), r = h->alloc_cf(B, Co, T, L, L);
+      float* edge = h->arena.alloc(fea_edge_floats(B * T, Cf, fs));
+      fill_normal(s, f.p, 1, (int)f.numel(), 17, 0, 0, 2);
+      fill_normal(s, r.p, 1, (int)r.numel(), 17, 0, 0, 1);
+      const auto& fw = h->Pfea_phase();
+      const PackedW& w5 = h->P("init_conv.weight#fea5");
+      ConvEpi e;
+      e.res = r.p; e.res_sb = r.sb; e.res_sc = r.sc; e.res_st = r.st;
+      const double pl = (double)B * T;
+      const double flop = layer == 0 ? pl * fs * fs * 2.0 * 4 * Co * Cf * 25
+                                     : pl * (2.0 * 4 * 8 * Co * 5 * Cf * fs + 2.0 * 4 * 16 * Co * Cf);
+      REQUIRE(conv_x3_phase_forward(s, r, f, w5, e, edge), "bench layer 0: phase conv rejected");  // the lines
+      std::function<void()> launch = [&, r, f, edge] {
+        if (layer == 0) REQUIRE(conv_x3_phase_forward(s, r, f, w5, e, edge), "bench layer 0: phase conv rejected");
+        else REQUIRE(fea_edges_forward(s, r, edge, Cf, fw.side, fw.side_scale, fw.corner), "bench layer 11: edges rejected");
+      };
+      launch();
+      hipEvent_t e0, e1;
+      HIPCHK(hipEventCreate(&e0));
+      HIPCHK(hipEventCreate(&e1));
+      HIPCHK(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; ++i) launch();
+      HIPCHK(hipEventRecord(e1, s));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      *ms_out = ms / iters;
+      *flops_out = flop;
+      return;
+    }
+    REQUIRE(layer != 11, "bench layer 11: the phase-composed cond_fea branch is off");
     static const char* names[] = {"init_conv.weight", "downs.0.0.block2.proj.weight", "downs.1.0.block2.proj.weight",
                                   "downs.2.0.block2.proj.weight", "ups.3.0.res_conv.weight",
                                   "downs.0.0.block2.proj.weight"};

@@ -15,6 +15,7 @@ state_dict key layout follow the reference, so reference checkpoints load with
 on a ROCm device; a CPU tensor is an error, not a fallback.
 """
 import dataclasses
+import warnings
 import math
 
 import torch
@@ -120,8 +121,10 @@ class Unet3D(nn.Module):
         cache = self.__dict__.setdefault('_natives', {})
         h = cache.get(ver)
         if h is None:
-            # weights or schedule changed: handles of the old state are stale
-            for k in [k for k in cache if k[:2] != ver[:2]]:
+            # weights or schedule changed: handles of the old state are stale; a handle of another
+            # batch, device or precision is dropped too (each owns a max_batch-sized workspace,
+            # 3.7 GB at BAIR B = 64): only handles differing in fea_size are kept side by side
+            for k in [k for k in cache if k[:5] != ver[:5]]:
                 del cache[k]
             while len(cache) >= self._NATIVE_CACHE:
                 del cache[next(iter(cache))]
@@ -269,6 +272,28 @@ class GaussianDiffusion(nn.Module):
         # drawn from torch's default generator so torch.manual_seed makes runs reproducible
         return int(torch.randint(0, 2 ** 62, (1,)).item())
 
+    _RANGE_MSG = 'reached |v| >= 65504'
+
+    def _run_sampler(self, B, device, fea_size, run):
+        """run(handle) on the denoiser's native handle. In f16x3 a conv operand at or past the
+        fp16 range (|v| >= 65504) makes the library reject the sampling call (runtime.cpp
+        extdm_sample); the call is then re-run on an FP32 handle (the exact fp32-MFMA kernels)
+        and the denoiser stays on FP32 from then on (a checkpoint that trips the guard once
+        keeps tripping it), logged once."""
+        fn = self.denoise_fn
+        if getattr(self, '_fp32_fallback', False) and fn.precision != 'fp32':
+            fn.precision = 'fp32'
+        try:
+            return run(self._native(B, device, fea_size))
+        except RuntimeError as e:
+            if self._RANGE_MSG not in str(e) or fn.precision == 'fp32':
+                raise
+            warnings.warn('ExtDM: f16x3 activations reached the fp16 range (|v| >= 65504); re-running '
+                          'the sampling call and continuing on the FP32 kernels', RuntimeWarning)
+            self._fp32_fallback = True
+            fn.precision = 'fp32'
+            return run(self._native(B, device, fea_size))
+
     @torch.inference_mode()
     def p_sample(self, x_cond, x, cond_fea, t, cond=None, cond_scale=1., clip_denoised=True, noise=None):
         """One ancestral step (Diffusion.py:169-177); noise defaults to
@@ -296,10 +321,10 @@ class GaussianDiffusion(nn.Module):
         B = shape[0]
         out = torch.empty(shape, device=device, dtype=torch.float32)
         times = list(reversed(range(self.num_timesteps)))
-        h = self._native(B, device, cond_fea.shape[-1])
-        h.sample(_lib.SAMPLER_DDPM, times, None, 0., x_cond.float().contiguous(), cond_fea.float().contiguous(), out,
-                 x_T=x_T, noise=noise, seed=self._seed() if seed is None else seed, sample_base=sample_base,
-                 round_idx=round_idx, use_graph=self.use_graph)
+        seed = self._seed() if seed is None else seed
+        self._run_sampler(B, device, cond_fea.shape[-1], lambda h: h.sample(
+            _lib.SAMPLER_DDPM, times, None, 0., x_cond.float().contiguous(), cond_fea.float().contiguous(), out,
+            x_T=x_T, noise=noise, seed=seed, sample_base=sample_base, round_idx=round_idx, use_graph=self.use_graph))
         return out
 
     @torch.no_grad()
@@ -311,11 +336,11 @@ class GaussianDiffusion(nn.Module):
         B = shape[0]
         pairs = ddim_time_pairs(self.num_timesteps, self.sampling_timesteps)
         out = torch.empty(shape, device=device, dtype=torch.float32)
-        h = self._native(B, device, cond_fea.shape[-1])
-        h.sample(_lib.SAMPLER_DDIM, [p[0] for p in pairs], [p[1] for p in pairs], self.ddim_sampling_eta,
-                 x_cond.float().contiguous(), cond_fea.float().contiguous(), out, x_T=x_T, noise=noise,
-                 seed=self._seed() if seed is None else seed, sample_base=sample_base, round_idx=round_idx,
-                 use_graph=self.use_graph)
+        seed = self._seed() if seed is None else seed
+        self._run_sampler(B, device, cond_fea.shape[-1], lambda h: h.sample(
+            _lib.SAMPLER_DDIM, [p[0] for p in pairs], [p[1] for p in pairs], self.ddim_sampling_eta,
+            x_cond.float().contiguous(), cond_fea.float().contiguous(), out, x_T=x_T, noise=noise, seed=seed,
+            sample_base=sample_base, round_idx=round_idx, use_graph=self.use_graph))
         return out
 
     @torch.inference_mode()

@@ -98,7 +98,7 @@ def parse(argv=None):
     ap.add_argument('--total-pred', type=int, default=None)
     ap.add_argument('--tp', type=int, default=None)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-steps', type=int, default=3, help='timed oracle steps per CPU batch point')
+    ap.add_argument('--cpu-steps', type=int, default=5, help='timed oracle steps per CPU batch point')
     ap.add_argument('--precision', default=None, choices=['fp32', 'f16x3', 'bf16_attn'],
                     help='conv / attention arithmetic (include/extdm.h EXTDM_PRECISION_*); default: package default')
     ap.add_argument('--no-roofline', action='store_true', help='test-only: skip the per-kernel roofline timing')
@@ -379,8 +379,8 @@ def cpu_model():
 
 
 def cpu_threads():
-    """Host cores this process may run on (sched affinity) and the threads the CPU
-    baseline uses: OMP_NUM_THREADS where set (the GPU box's per-GPU CPU share), else all."""
+    """Host cores this process may run on (sched affinity), and the OMP_NUM_THREADS slice
+    where one is set (the GPU box's per-GPU CPU share; else all cores)."""
     cores = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
     env = os.environ.get('OMP_NUM_THREADS')
     threads = min(cores, int(env)) if env and env.isdigit() and int(env) > 0 else cores
@@ -389,13 +389,16 @@ def cpu_threads():
 
 def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
     """The oracle (PyTorch-CPU restatement of the reference, kind "port") timed on this
-    box's host cores at B = 1 and at a steady batch: one round's LFAE
-    encoder and decode (B = 1, scaled by B), n_steps reverse steps (Unet forward + the
-    DDPM / DDIM update) per batch point, extrapolated to the workload's rounds x steps;
-    the better batch point is `value`. Oracle use is confined to this untimed leg."""
+    box's host cores (torch.set_num_threads(<all host cores>))
+    at B = 1 and at a steady batch: one round's LFAE encoder and decode (B = 1, scaled by B),
+    n_steps reverse steps (Unet forward + the DDPM / DDIM update; median, with the spread)
+    per batch point, extrapolated to the workload's rounds x steps. `value` = the better
+    all-cores batch point; where OMP_NUM_THREADS sets a smaller slice, B = 1 is also timed on
+    that slice (reported beside it, not the value). Oracle use is confined to this untimed leg."""
     from oracle import extdm_oracle as O
     from oracle import lfae_oracle as LO
-    cores, threads = cpu_threads()
+    cores, slice_threads = cpu_threads()
+    threads = cores
     torch.set_num_threads(threads)
     ucfg = fd.unet.ucfg
     lc = fd.lcfg
@@ -417,11 +420,16 @@ def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
         t0 = time.perf_counter()
         LO.decode_round(sd, lc, ucfg, ret, x, ref)
         t_dec = time.perf_counter() - t0
+        pairs = O.ddim_pairs(T_sched, steps_per_round) if ddim else None
+        # a warm step + n_steps timed ones, all inside the sampler's step list
+        n_steps = max(1, min(n_steps, (len(pairs) if ddim else T_sched) - 1))
+        runs = [(threads, B) for B in ([1, steady_batch] if steady_batch > 1 else [1])]
+        if slice_threads < threads:
+            runs.append((slice_threads, 1))
         points = []
-        for B in ([1, steady_batch] if steady_batch > 1 else [1]):
+        for nth, B in runs:
+            torch.set_num_threads(nth)
             xc, fb, xb = x_cond.expand(B, *x_cond.shape[1:]), fea.expand(B, *fea.shape[1:]), x.expand(B, *x.shape[1:])
-
-            pairs = O.ddim_pairs(T_sched, steps_per_round) if ddim else None
 
             def step(k, xb):
                 ti = pairs[k][0] if ddim else T_sched - 1 - k
@@ -438,16 +446,21 @@ def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
                 per.append(time.perf_counter() - t0)
             t_step = float(np.median(per))
             total = rounds * B * (t_enc + t_dec) + rounds * steps_per_round * t_step
-            points.append({'batch': B, 'frames_per_s': round(rounds * ucfg.tp * B / total, 5),
-                           's_per_step': round(t_step, 4)})
-    best = max(points, key=lambda p: p['frames_per_s'])
+            points.append({'threads': nth, 'batch': B, 'frames_per_s': round(rounds * ucfg.tp * B / total, 5),
+                           's_per_step': round(t_step, 4), 's_per_step_min_max': [round(min(per), 4), round(max(per), 4)]})
+        torch.set_num_threads(threads)
+    best = max((p for p in points if p['threads'] == threads), key=lambda p: p['frames_per_s'])
     return {'value': best['frames_per_s'], 'unit': 'frames/s', 'cores': cores, 'threads': threads,
             'kind': 'port', 'cpu_model': cpu_model(), 'batch_points': points,
-            'sample': f'oracle (PyTorch-CPU fp32) on {threads} threads of {cores} host cores: encoder round '
+            'baseline_method': 'r04: all host cores (value) + the OMP_NUM_THREADS slice at B=1; median of '
+                               f'{n_steps} timed steps per point (r03: the OMP slice only, 3 steps)',
+            'sample': f'oracle (PyTorch-CPU fp32) on {threads} threads = all {cores} host cores: encoder round '
                       f'({t_enc:.3f} s) and decode round ({t_dec:.3f} s) at B=1, {n_steps} '
                       f'{"DDIM" if ddim else "DDPM"} steps per batch point (B = '
-                      f'{", ".join(str(p["batch"]) for p in points)}); extrapolated to {rounds} rounds x '
-                      f'{steps_per_round} steps; value = the better batch point (B={best["batch"]})'}
+                      f'{", ".join(str(p["batch"]) for p in points if p["threads"] == threads)}'
+                      + (f'; B=1 also on the {slice_threads}-thread OMP_NUM_THREADS slice' if slice_threads < threads else '')
+                      + f'); extrapolated to {rounds} rounds x {steps_per_round} steps; value = the better '
+                      f'all-cores batch point (B={best["batch"]})'}
 
 
 # ------------------------------------------------------------------ rank body

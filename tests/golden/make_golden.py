@@ -198,6 +198,30 @@ def wrappers():
     np.savez_compressed(os.path.join(HERE, 'wrappers.npz'), **out)
 
 
+def ddpm1000():
+    """A whole DDPM-1000 chain (the headline metric's sampler length) through the reference's
+    own p_sample (the evident binding; Diffusion.py:180-189 raises as written) on the reduced
+    u12 denoiser, with x after selected steps (tests/golden/ddpm1000.npz)."""
+    from tests.golden_inputs import ddpm1000_case, DDPM1000_SNAPS
+    from model.BaseDM_adaptor.Diffusion import GaussianDiffusion
+    cfg, x, cond, fea, seed = ddpm1000_case()
+    Unet3D, _, _ = import_reference()
+    net = build_ref_unet(Unet3D, cfg)
+    net.load_state_dict(make_sd(cfg), strict=True)
+    d = GaussianDiffusion(net, image_size=cfg.latent, num_frames=cfg.tc + cfg.tp, timesteps=1000,
+                          sampling_timesteps=1000, null_cond_prob=0.0)
+    torch.manual_seed(seed)
+    img = torch.randn(x.shape)
+    out = {}
+    with torch.no_grad():
+        for i in reversed(range(1000)):
+            img = d.p_sample(cond, img, fea, torch.full((x.shape[0],), i, dtype=torch.long))
+            if i in DDPM1000_SNAPS:
+                out[f'x_after_{i}'] = img.numpy()
+                print('ddpm1000 t', i, float(img.abs().max()), flush=True)
+    np.savez_compressed(os.path.join(HERE, 'ddpm1000.npz'), **out)
+
+
 def e2e():
     """End-to-end sampling at the other BASELINE configs' shapes (tests/golden/e2e.npz;
     tests/golden_inputs.py E2E): KTH DDIM-100 (ada), Cityscapes 5 DDPM steps (ada_u22,
@@ -440,6 +464,11 @@ def metrics():
 
 
 if __name__ == '__main__':
+    if '--ddpm1000' in sys.argv:
+        torch.set_num_threads(8)
+        import_reference()
+        ddpm1000()
+        sys.exit(0)
     if '--metrics' in sys.argv:
         import_reference()
         metrics()

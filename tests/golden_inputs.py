@@ -102,6 +102,18 @@ def ddpm100_case():
     return cfg, x, cond, fea, 47
 
 
+def ddpm1000_case():
+    """The metric's sampler length (BASELINE: DDPM 1000 steps) on the reduced u12 denoiser (the
+    BAIR module at dim 16): x_T and one draw per step from torch.manual_seed(seed), t = 999..0
+    (p_sample draws at t = 0 too), snapshots of x after the steps listed in DDPM1000_SNAPS."""
+    cfg = CONFIGS['small']
+    x, _, cond, fea = unet_inputs(cfg, B=2, seed=31)  # B = 1 trips a view in the reference STW at 2x2 levels
+    return cfg, x, cond, fea, 61
+
+
+DDPM1000_SNAPS = [999, 900, 500, 100, 10, 0]  # x after the step at these t
+
+
 def ddim_noise(shape, S=10):
     """The CPU noise stream one reference ddim_sample consumes after torch.manual_seed:
     x_T, then a draw for every step whose time_next > 0 (Diffusion.py:217, 250); the

@@ -62,3 +62,44 @@ def test_attention_layer_vs_oracle(prefix, level, shifted, precision, monkeypatc
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), out2.cpu())
     assert err <= 2e-5, err
+
+
+@pytest.mark.parametrize('prefix,level,shifted', [('downs.0.1', 0, True), ('downs.2.3', 2, False),
+                                                  ('init_temporal_attn', 0, None)])
+def test_attention_core_heads6_vs_oracle(prefix, level, shifted):
+    """heads = 6 (heads % 4 != 0): the f16x3 attention core walks heads over 4 waves per block,
+    so two waves get a second head and two do not (the round-2 ADVICE wave-barrier fix,
+    attn_core.hip: no block barrier inside the head loop). The fused kernels take heads = 8
+    only, so every attention layer of this config runs the unfused route through the core."""
+    import dataclasses
+    from oracle import extdm_oracle as O
+    cfg = dataclasses.replace(CONFIGS['bair'], heads=6)
+    key = ('bair_h6', 'f16x3')
+    if key not in _H:
+        h = pkg._lib.Handle(cfg, 1000, 2, 0, precision='f16x3')
+        sd = make_sd(cfg)
+        sd.update(pkg.schedule_buffers(1000))
+        h.load_state(sd)
+        h.finalize()
+        _H[key] = (h, sd)
+    h, sd = _H[key]
+    C = cfg.dim * (1 if level == 0 else cfg.dim_mults[level])
+    L = cfg.latent >> level
+    gen = torch.Generator().manual_seed(15 + level)
+    x = torch.randn(2, C, cfg.frames, L, L, generator=gen) * 1.5 + 0.3
+    out = torch.empty(x.shape, device=DEV)
+    h.attn_layer(prefix, x.to(DEV), out, shifted=bool(shifted))
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        if shifted is None:
+            ref = O.temporal_attention(sd, prefix, x, O.time_pos_bias(sd, cfg.frames), cfg.heads, cfg.dim_head)
+        else:
+            win = tuple(cfg.window)
+            ref = O.stw_attention(sd, prefix, x, win, tuple(w // 2 for w in win) if shifted else (0, 0, 0),
+                                  cfg.heads, cfg.dim_head)
+    err = (out.cpu() - ref).abs().max().item()
+    out2 = torch.empty(x.shape, device=DEV)
+    h.attn_layer(prefix, x.to(DEV), out2, shifted=bool(shifted))
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), out2.cpu())
+    assert err <= 2e-5, err

@@ -315,3 +315,69 @@ def test_drop_in_api_sample_shapes_and_determinism():
     b = d.sample(cond.to(DEV), cond_fea=fea.to(DEV))
     assert a.shape == (2, 3, cfg.tp, cfg.latent, cfg.latent)
     assert torch.equal(a, b) and torch.isfinite(a).all()
+
+
+def test_range_guard_falls_back_to_fp32():
+    """f16x3 rejects a sampling call whose conv operands reach |v| >= 65504 (runtime.cpp
+    extdm_sample); GaussianDiffusion then re-runs it on an FP32 handle: the
+    result equals an explicit FP32 run with the same seed, and the warning is raised."""
+    cfg = CONFIGS['small']
+
+    def make(precision):
+        u = pkg.Unet3D(dim=cfg.dim, channels=512, dim_mults=cfg.dim_mults, cond_num=cfg.tc, pred_num=cfg.tp,
+                       framesize=cfg.latent).to(DEV)
+        u.precision = precision
+        return pkg.GaussianDiffusion(u, image_size=cfg.latent, num_frames=cfg.tc + cfg.tp, timesteps=1000,
+                                     sampling_timesteps=3).to(DEV)
+    _, _, cond, fea = unet_inputs(cfg)
+    fea = (fea * 1e5).to(DEV)  # TrajWarp's k / v projection inputs past the fp16 range
+    d16 = make('f16x3')
+    with pytest.warns(RuntimeWarning, match='65504'):
+        a = d16.ddim_sample(cond.to(DEV), (2, 3, cfg.tp, cfg.latent, cfg.latent), fea, seed=11)
+    assert d16.denoise_fn.precision == 'fp32'
+    b = make('fp32').ddim_sample(cond.to(DEV), (2, 3, cfg.tp, cfg.latent, cfg.latent), fea, seed=11)
+    assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))
+
+
+@pytest.mark.parametrize('precision', ['f16x3', 'fp32'])
+def test_ddpm1000_chain_vs_reference_golden(precision):
+    """The headline metric's sampler length: a whole DDPM-1000 chain (t = 999 .. 0, the graph
+    replay path) against the reference's own p_sample loop on the reduced u12 denoiser, with
+    the reference's CPU noise stream injected (tests/golden/ddpm1000.npz, make_golden.py
+    ddpm1000). Checked at the snapshots after t = 999, 900, 500, 100, 10 and 0 by running the
+    chain piecewise from the golden state, and as one 1000-step chain from x_T. Bar: the
+    single-step bar (1e-4, test_ddpm_steps_vs_reference_golden) plus 2e-6 per step of the
+    segment (the survey's drift contract, 7.4e-7 per 10 steps, with margin): 2.1e-3 for the
+    whole chain."""
+    from tests.golden_inputs import ddpm1000_case, DDPM1000_SNAPS
+    cfg, x, cond, fea, seed = ddpm1000_case()
+    g = load('ddpm1000.npz')
+    h = pkg._lib.Handle(cfg, 1000, x.shape[0], 0, precision=precision)
+    sd = make_sd(cfg)
+    sd.update(pkg.schedule_buffers(1000))
+    h.load_state(sd)
+    h.finalize()
+    torch.manual_seed(seed)
+    xT = torch.randn(x.shape)
+    noises = torch.stack([torch.randn(x.shape) for _ in range(1000)])  # p_sample draws at every t
+    cd, fd = cond.to(DEV), fea.to(DEV)
+    out = torch.empty(x.shape, device=DEV)
+    h.sample(0, list(range(999, -1, -1)), None, 0., cd, fd, out, x_T=xT.to(DEV), noise=noises.to(DEV).contiguous(),
+             use_graph=True)
+    torch.cuda.synchronize()
+    whole = np.abs(out.cpu().numpy() - g['x_after_0']).max()
+    # piecewise: each segment restarted from the golden state (isolates per-segment error)
+    seg = {}
+    prev, start = xT, 999
+    for ts in DDPM1000_SNAPS:
+        times = list(range(start, ts - 1, -1))
+        nz = noises[999 - start: 999 - ts + 1]
+        h.sample(0, times, None, 0., cd, fd, out, x_T=prev.to(DEV), noise=nz.to(DEV).contiguous(), use_graph=True)
+        torch.cuda.synchronize()
+        ref = g[f'x_after_{ts}']
+        seg[ts] = (len(times), float(np.abs(out.cpu().numpy() - ref).max()))
+        prev, start = torch.from_numpy(ref), ts - 1
+    print(precision, 'whole chain max|diff|', whole, 'segments (steps, max|diff|)', seg)
+    for ts, (n, e) in seg.items():
+        assert e <= 1e-4 + 2e-6 * n, (ts, n, e)
+    assert whole <= 1e-4 + 2e-6 * 1000, whole
