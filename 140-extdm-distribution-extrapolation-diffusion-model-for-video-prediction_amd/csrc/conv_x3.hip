@@ -28,6 +28,20 @@
 
 #include "kernels.h"
 
+// EXTDM_X3_LIN: the staged (fp32-input) X tile of the one-group tiles in the operand layout
+// [hl][c8][pos][8] (a lane's k-slice = one 16-B record, consecutive positions = consecutive
+// records: conflict-free ds_read_b128 with no swizzle, and a kx step is an immediate offset)
+// instead of [hl][pos][16] with the bit-3 swizzle
+#ifndef EXTDM_X3_LIN
+#define EXTDM_X3_LIN 0
+#endif
+// EXTDM_X3_BUFX: the staged X loads as buffer loads (the lane's pixel offset in VGPR, the
+// channel's offset in soffset, a position outside the image past the extent so the load itself
+// returns 0): no 64-bit address VALU per load and no store-time position mask
+#ifndef EXTDM_X3_BUFX
+#define EXTDM_X3_BUFX 0
+#endif
+
 namespace extdm {
 
 __device__ int g_x3_range;
@@ -54,6 +68,8 @@ struct X3Args {
   // PH: F's four edge lines [P][4 (top, bottom, left, right)][W][Cin] (fp32), written by the
   // m-tile-0 workgroups while staging (fea_x3.hip reads them); null: not written
   float* edge;
+  int mfast;
+  int in0_bytes, in1_bytes;  // BUFX: byte extents of the two sources (< 2^30), 0 = not usable
   ConvEpi e;
 };
 
@@ -140,8 +156,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   extern __shared__ __attribute__((aligned(16))) _Float16 smx[];
   // halves from an X slot's hi block to its lo block (DMA mode: two c8 planes of whole
   // 1 KiB pieces each)
-  const int XPL = ((a.XPOS + 63) & ~63) * 8;  // DMA mode: halves per (hl, c8) plane
-  const int XLO = XOP ? 2 * XPL : NG * a.XPOS * 16;
+  constexpr bool LIN = EXTDM_X3_LIN && NG == 1 && !XOP;
+  // halves per (hl, c8) plane: DMA mode whole 1 KiB pieces; LIN one spare position past XPOS
+  // (the target of unused staging slots)
+  const int XPL = ((a.XPOS + (LIN ? 1 : 0) + 63) & ~63) * 8;
+  const int XLO = (XOP || LIN) ? 2 * XPL : NG * a.XPOS * 16;
   const int XH = 2 * XLO;  // halves per X slot (hi + lo)
   _Float16* As0 = smx;
   _Float16* As1 = smx + AHS;
@@ -158,11 +177,24 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   // XCDs). PMC at B = 64: 7x7 2326 -> 2062 MB, level-0 3x3 599 -> 546 MB per launch. The 1x1
   // tiles share nothing across tiles and ran 5 % slower remapped (HBM-bound: the round-robin
   // order spreads the 8 XCDs' concurrent reads over neighbouring addresses).
-  const int tile = (KS == 1 || (gridDim.x & 7)) ? (int)blockIdx.x
-                                                : (int)((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3));
+  // MFAST (1x1 with all m-tiles' weights within an XCD's L2, host: x3_mfast): the k-th
+  // workgroup of XCD x takes m-tile k % MT of pixel tile x + 8 (k / MT), so a pixel tile's MT
+  // m-tiles run back to back on one XCD and its input is read from HBM once (the default
+  // order re-read it once per m-tile: the ups.3 Tmodulator 7 x 235 MB)
+  int tile, mtile;
+  if (KS == 1 && a.mfast) {
+    const int lin = (int)(blockIdx.x + gridDim.x * blockIdx.y), MT = (int)gridDim.y;
+    const int k = lin >> 3;
+    mtile = k % MT;
+    tile = (lin & 7) + 8 * (k / MT);
+  } else {
+    tile = (KS == 1 || (gridDim.x & 7)) ? (int)blockIdx.x
+                                        : (int)((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3));
+    mtile = blockIdx.y;
+  }
   const int plane0 = (tile / a.nrow_tiles) * a.NP;
   const int row0 = (tile % a.nrow_tiles) * a.TH;
-  const int mtile = blockIdx.y;
+
   const int THK = a.TH + KS - 1;
   // first halo position of the tile in the operand's padded [P][H+KS-1][RS] planes
   const int tb = (plane0 * (a.H + KS - 1) + row0) * a.RS;
@@ -203,7 +235,25 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   const int gC0 = a.C0, gCin = a.Cin;
   // channel groups never straddle the two sources nor run past Cin (wave-uniform)
   const bool whole = gC0 % 16 == 0 && gCin % CIB == 0;
+  const bool bufx = EXTDM_X3_BUFX && whole && a.in0_bytes > 0;
+  const auto rsx0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in0), 0, a.in0_bytes, 0x00020000);
+  const auto rsx1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in1), 0, a.in1_bytes, 0x00020000);
   auto load_x_exact = [&](int cgb) __attribute__((always_inline)) {
+    if (bufx) {
+#pragma unroll
+      for (int j = 0; j < NSLOT; ++j) {
+        // the slot's channel group is wave-uniform (host: one group, or XPOS % 64 == 0)
+        const int ci0 = __builtin_amdgcn_readfirstlane(cgb * CIB + (sg[j] < 0 ? 0 : sg[j]) * 16);
+        const bool s1 = ci0 >= gC0;
+        const int vo = soff0[j] >= 0 ? (s1 ? soff1[j] : soff0[j]) * 4 : 0x40000000;
+        const int cb = s1 ? ci0 - gC0 : ci0;
+        const int cs4 = (int)(s1 ? gi1c : gi0c) * 4;
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+          xr[j][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(s1 ? rsx1 : rsx0, vo, (cb + c) * cs4, 0));
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < NSLOT; ++j) {  // every slot loads (unused ones a masked dummy): 16 * NSLOT loads
       const bool pos_ok = soff0[j] >= 0;
@@ -284,7 +334,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
           // pinned here (volatile: not hoisted above the stage barriers of the 7x7
           // ky loop, where the first use of a load result would wait for the X loads)
           asm volatile("" : "+v"(r));
-          r *= xmask(j, cgb, c);
+          if (!bufx) r *= xmask(j, cgb, c);  // bufx: outside positions already loaded as 0
         }
         v[c] = r;
       }
@@ -300,8 +350,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
       const h8 hi1 = __builtin_bit_cast(h8, u32x4{hw[4], hw[5], hw[6], hw[7]});
       const h8 lo0 = __builtin_bit_cast(h8, u32x4{lw[0], lw[1], lw[2], lw[3]});
       const h8 lo1 = __builtin_bit_cast(h8, u32x4{lw[4], lw[5], lw[6], lw[7]});
-      const int sw = (spos[j] >> 3) & 1;
       const bool used = sg[j] >= 0;
+      if (LIN) {
+        _Float16* d = Xs + (used ? spos[j] : XPL / 8 - 1) * 8;
+        *reinterpret_cast<h8*>(d) = hi0;
+        *reinterpret_cast<h8*>(d + XPL) = hi1;
+        *reinterpret_cast<h8*>(d + 2 * XPL) = lo0;
+        *reinterpret_cast<h8*>(d + 3 * XPL) = lo1;
+        continue;
+      }
+      const int sw = (spos[j] >> 3) & 1;
       _Float16* dh = used ? Xs + ((long)sg[j] * a.XPOS + spos[j]) * 16 : xdummy;
       _Float16* dl = used ? dh + XLO : xdummy + 16;
       *reinterpret_cast<h8*>(dh + 8 * sw) = hi0;
@@ -404,11 +462,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
       const int ix = line == 2 ? 0 : (line == 3 ? a.W - 1 : jj);
       if (q >= a.P || iy < row0 || iy >= row0 + a.TH) continue;
       const int pos = (pp * THK + iy - row0 + PAD) * a.RS + ix + PAD;
-      const int sw = (pos >> 3) & 1;
-      const _Float16* xh = Xs + (long)pos * 16;
-      const h8 h0 = *reinterpret_cast<const h8*>(xh + 8 * sw), h1 = *reinterpret_cast<const h8*>(xh + 8 * (sw ^ 1));
-      const h8 l0 = *reinterpret_cast<const h8*>(xh + XLO + 8 * sw);
-      const h8 l1 = *reinterpret_cast<const h8*>(xh + XLO + 8 * (sw ^ 1));
+      h8 h0, h1, l0, l1;
+      if (LIN) {
+        const _Float16* xh = Xs + (long)pos * 8;
+        h0 = *reinterpret_cast<const h8*>(xh);
+        h1 = *reinterpret_cast<const h8*>(xh + XPL);
+        l0 = *reinterpret_cast<const h8*>(xh + 2 * XPL);
+        l1 = *reinterpret_cast<const h8*>(xh + 3 * XPL);
+      } else {
+        const int sw = (pos >> 3) & 1;
+        const _Float16* xh = Xs + (long)pos * 16;
+        h0 = *reinterpret_cast<const h8*>(xh + 8 * sw);
+        h1 = *reinterpret_cast<const h8*>(xh + 8 * (sw ^ 1));
+        l0 = *reinterpret_cast<const h8*>(xh + XLO + 8 * sw);
+        l1 = *reinterpret_cast<const h8*>(xh + XLO + 8 * (sw ^ 1));
+      }
       float v[16];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -453,8 +521,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int pos = bpos[j] + ky * a.RS + kx;
-          const _Float16* bp = XOP ? Xs + h * XPL + pos * 8
-                                   : Xs + ((long)g * a.XPOS + pos) * 16 + 8 * (h ^ ((pos >> 3) & 1));
+          const _Float16* bp = (XOP || LIN) ? Xs + h * XPL + pos * 8
+                                            : Xs + ((long)g * a.XPOS + pos) * 16 + 8 * (h ^ ((pos >> 3) & 1));
           bh[j] = *reinterpret_cast<const h8*>(bp);
           bl[j] = *reinterpret_cast<const h8*>(bp + XLO);
         }
@@ -661,7 +729,9 @@ template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool
           bool RGN = false, int SPL = 0, bool PH = false>
 void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
   constexpr int AH = KY * NG * KS * (BM / 32) * 2 * 512;
-  const size_t xlo = XOP ? (size_t)((a.XPOS + 63) & ~63) * 16 : (size_t)a.XPOS * NG * 16;
+  constexpr bool LIN = EXTDM_X3_LIN && NG == 1 && !XOP;
+  const size_t xlo = XOP ? (size_t)((a.XPOS + 63) & ~63) * 16
+                         : (LIN ? (size_t)((a.XPOS + 1 + 63) & ~63) * 16 : (size_t)a.XPOS * NG * 16);
   // + 32 halves (unused-slot dummy) + 2 * BM floats (epilogue scale / bias)
   const size_t lds = ((size_t)2 * AH + (size_t)XBUF * 2 * xlo + 32 + 4 * BM) * sizeof(_Float16);
   dim3 grid(ntiles, (a.Cout + BM - 1) / BM, SPL == 1 ? a.nsplit : 1);
@@ -697,13 +767,16 @@ void launch_ns(hipStream_t s, const X3Args& a, unsigned ntiles) {
 // the 1x1 128-row tile (several workgroups per CU) splits below 384, up to 512. Slices keep
 // >= 2 channel blocks. The slice count is a function of the per-sample geometry only (the
 // workgroup count at the reference batch 64), never of the batch: a clip's result must
-// not depend on the shard it lands in (tiles never straddle samples here, T % NP == 0).
-// EXTDM_NO_SPLITK=1 turns it off (A/B).
-int split_slices(const X3Args& a, unsigned ntiles, long max_wg, long max_total) {
+// not depend on the shard it lands in (every output element sums the same slices in the same
+// order whichever tile, and whichever tile-mates, it has). EXTDM_NO_SPLITK=1 turns it off (A/B).
+int split_slices(const X3Args& a, unsigned ntiles, long max_wg, long max_total, int bm = 128) {
   static const bool off = [] { const char* v = getenv("EXTDM_NO_SPLITK"); return v && v[0] && v[0] != '0'; }();
-  const int B = a.P / a.T;
-  if (off || a.ncgb < 4 || a.T % a.NP != 0 || B < 1 || (long)ntiles % B != 0) return 0;
-  const long nwg64 = (long)ntiles / B * ((a.Cout + 127) / 128) * 64;
+  (void)ntiles;
+  if (off || a.ncgb < 4 || a.P < 1) return 0;
+  // workgroups of this conv at the reference batch 64 (a function of the per-sample geometry:
+  // T frames per sample, NP planes and nrow_tiles row tiles per tile; single-frame views such as
+  // the Tmodulator's '(T C)' GEMM put several samples in one tile, which is still batch-independent)
+  const long nwg64 = (64L * a.T + a.NP - 1) / a.NP * a.nrow_tiles * ((a.Cout + bm - 1) / bm);
   if (nwg64 >= max_wg) return 0;
   const int S = (int)std::min<long>(a.ncgb / 2, max_total / nwg64);
   return S >= 2 ? S : 0;
@@ -711,8 +784,15 @@ int split_slices(const X3Args& a, unsigned ntiles, long max_wg, long max_total) 
 size_t split_bytes(const X3Args& a, unsigned ntiles, int S) {
   return S ? (size_t)S * ntiles * ((a.Cout + 127) / 128) * 128 * 128 * sizeof(float) : 0;
 }
-bool split_k(X3Args& a, unsigned ntiles, const ConvEpi& e, long max_wg, long max_total) {
-  const int S = split_slices(a, ntiles, max_wg, max_total);
+// The 256-row 1x1 tile (one workgroup per CU) splits below 256 workgroups, into at most 256:
+// the level-3 / mid Tmodulators ('(T C)' = 3584 input channels, 112 workgroups at B = 64).
+// EXTDM_X3_SPLIT256=0 turns it off (A/B).
+bool x3_split256() {
+  static const bool on = [] { const char* v = getenv("EXTDM_X3_SPLIT256"); return !(v && v[0] == '0'); }();
+  return on;
+}
+bool split_k(X3Args& a, unsigned ntiles, const ConvEpi& e, long max_wg, long max_total, int bm = 128) {
+  const int S = split_slices(a, ntiles, max_wg, max_total, bm);
   if (!S || !e.split_ws || split_bytes(a, ntiles, S) > e.split_ws_bytes) return false;
   a.part = e.split_ws;
   a.nsplit = S;
@@ -731,7 +811,8 @@ bool x3_w128_4(const X3Args& a, bool xop) {
   static const int w = [] { const char* v = getenv("EXTDM_X3_W128"); return v ? atoi(v) : 4; }();
   if (w == 8) return false;
   constexpr size_t AH = 3 * 4 * 2 * 512;
-  const size_t xlo = xop ? (size_t)((a.XPOS + 63) & ~63) * 16 : (size_t)a.XPOS * 16;
+  const size_t xlo = xop ? (size_t)((a.XPOS + 63) & ~63) * 16
+                         : (EXTDM_X3_LIN ? (size_t)((a.XPOS + 1 + 63) & ~63) * 16 : (size_t)a.XPOS * 16);
   return (2 * AH + 2 * 2 * xlo + 32 + 4 * 128) * sizeof(_Float16) <= 80 * 1024;
 }
 // split-K thresholds of the 3x3 128-row tile (launch_wg, total_wg): 8 waves at one workgroup
@@ -824,6 +905,17 @@ bool x3_setup(const View& out, const View& in0, const View* in1, const PackedW& 
   a.out_bytes = (int)ob;
   a.res_bytes = (int)rb;
   ntiles = (unsigned)(((a.P + a.NP - 1) / a.NP) * a.nrow_tiles);
+  // BUFX: both sources' byte extents below 2^30 (the out-of-image offset 2^30 then reads 0)
+  // and the staging slots' channel group wave-uniform
+  {
+    auto ext_in = [&](const View& v) {
+      return ((long)(v.B - 1) * v.sb + (long)(v.C - 1) * v.sc + (long)(v.T - 1) * v.st + (long)v.H * v.W) * 4;
+    };
+    const long e0 = ext_in(in0), e1 = in1 ? ext_in(*in1) : e0;
+    const bool ok = e0 < (1L << 30) && e1 < (1L << 30) && (tl.ng == 1 || a.XPOS % 64 == 0);
+    a.in0_bytes = ok ? (int)e0 : 0;
+    a.in1_bytes = ok ? (int)e1 : 0;
+  }
   // GroupNorm partials in the epilogue: whole tiles inside one sample, groups of whole
   // 8-row blocks inside one m-tile, at most 64 slots (the runtime's partials buffer)
   if (epi.stats) {
@@ -843,6 +935,16 @@ bool x3_setup(const View& out, const View& in0, const View* in1, const PackedW& 
 
 }  // namespace
 
+// 1x1: the m-tile-fast XCD order (kernel note MFAST) when the whole weight (every m-tile, hi +
+// lo) fits comfortably in one XCD's 4 MiB L2 and there is more than one m-tile.
+// EXTDM_X3_NO_MFAST=1 turns it off (A/B).
+bool x3_mfast(const X3Args& a, const X3Tile& tl, unsigned ntiles) {
+  static const bool off = [] { const char* v = getenv("EXTDM_X3_NO_MFAST"); return v && v[0] && v[0] != '0'; }();
+  static const long cap = [] { const char* v = getenv("EXTDM_X3_MFAST_KB"); return (v ? atol(v) : 3584L) * 1024; }();
+  const long mt = (a.Cout + tl.bm - 1) / tl.bm;
+  return !off && mt > 1 && ntiles % 8 == 0 && mt * tl.bm * (long)a.Cin * 4 <= cap;
+}
+
 bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                      const ConvEpi& epi, int* stats_slots) {
   X3Args a;
@@ -850,6 +952,7 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
   if (!x3_setup(out, in0, in1, w, epi, a, ntiles, stats_slots)) return false;
   const int ks = w.KH;
   const X3Tile tl{w.xbm, w.xbn, w.xng};
+  if (ks == 1) a.mfast = x3_mfast(a, tl, ntiles);
   if (epi.res_aff) {  // residual GroupNorm: the 1x1 tiles only
     if (ks != 1 || !epi.res || tl.bn != 128) return false;
     if (tl.bm == 64) launch_sp<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, true>(s, a, ntiles);
@@ -895,7 +998,14 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     }
   }
   else if (ks == 1 && tl.bm == 64) launch<1, 1, 64, 128, 2, 4, 4, 2>(s, a, ntiles);
-  else if (ks == 1 && tl.bm == 256) launch<1, 1, 256, 128, 2, 2, 8, 2>(s, a, ntiles);
+  else if (ks == 1 && tl.bm == 256) {
+    if (x3_split256() && split_k(a, ntiles, epi, 256, 256, 256)) {
+      launch_sp<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 1>(s, a, ntiles);
+      launch_sp<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 2>(s, a, ntiles);
+    } else {
+      launch<1, 1, 256, 128, 2, 2, 8, 2>(s, a, ntiles);
+    }
+  }
   else if (ks == 1 && tl.bm == 128) {
     if (split_k(a, ntiles, epi, 384, 512)) {
       launch_sp<1, 1, 128, 128, 2, 2, 4, 2, true, 1, false, false, 1>(s, a, ntiles);
@@ -957,11 +1067,16 @@ bool conv_x3_covers(const View& out, const View& in0, const View* in1, const Pac
   return tile_ok && x3_setup(out, in0, in1, w, ConvEpi{}, a, ntiles, nullptr);
 }
 
+static size_t conv_x3_split_bytes_256(const X3Args& a, unsigned ntiles) {
+  return x3_split256() ? split_bytes(a, ntiles, split_slices(a, ntiles, 256, 256, 256)) : 0;
+}
+
 size_t conv_x3_split_bytes(const View& out, const View& in0, const View* in1, const PackedW& w) {
   X3Args a;
   unsigned ntiles = 0;
   if (w.mode != MODE_CONV || w.KH != w.KW || !x3_setup(out, in0, in1, w, ConvEpi{}, a, ntiles, nullptr)) return 0;
-  if (w.xbn == 512 || w.xbm != 128) return 0;
+  if (w.xbn == 512 || (w.xbm != 128 && !(w.xbm == 256 && w.KH == 1))) return 0;
+  if (w.xbm == 256) return conv_x3_split_bytes_256(a, ntiles);
   if (w.KH == 3) {
     long mw, mt;
     x3_split128(x3_w128_4(a, false), mw, mt);

@@ -174,38 +174,66 @@ __global__ __launch_bounds__(SNW * 64) void fea_side_x3_kernel(FeaSideArgs a) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       // rows of this lane: channel c = m >> 3 for r >> 2 = 0..3, phase (d = h, py, px) = r & 3
-      int off[8];
-      float2 rv[8];
+      if (a.pair == 0) {
+        // rows y = base + 2h + py: a lane owns the pixel pair x = 2jj, 2jj + 1 (8 B; the 32 lanes
+        // of a half cover 256 contiguous bytes of the row)
+        int off[8];
+        float2 rv[8];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int m0 = mtile * SBM + (wm * TM + i) * 32 + 8 * g + 4 * h;  // (py, px) = (0, 0)
-        const int c = m0 >> 3;
+        for (int g = 0; g < 4; ++g) {
+          const int c = (mtile * SBM + (wm * TM + i) * 32 + 8 * g) >> 3;
 #pragma unroll
-        for (int py = 0; py < 2; ++py) {
-          // the pair (px = 0, 1) is two adjacent pixels: x (pair 0) or ... (pair 1: x = base + 2d + px)
-          int y, x;
-          if (a.pair == 0) {
-            y = (side ? a.OH - 4 : 0) + 2 * h + py;
-            x = 2 * jj;
-          } else {
-            x = (side ? a.OW - 4 : 0) + 2 * h;
-            y = 2 * jj + py;
+          for (int py = 0; py < 2; ++py) {
+            const int k = 2 * g + py;
+            const int y = (side ? a.OH - 4 : 0) + 2 * h + py, x = 2 * jj;
+            off[k] = valid && c < a.Co ? (base + (int)(c * a.oc) + y * a.OW + x) * 4 : a.out_bytes;
+            const u32x2 ld = __builtin_amdgcn_raw_buffer_load_b64(rs, off[k], 0, 0);
+            rv[k] = make_float2(__uint_as_float(ld.x), __uint_as_float(ld.y));
           }
-          const int k = 2 * g + py;
-          off[k] = valid && c < a.Co ? (base + (int)(c * a.oc) + y * a.OW + x) * 4 : a.out_bytes;
-          const u32x2 ld = __builtin_amdgcn_raw_buffer_load_b64(rs, off[k], 0, 0);
-          rv[k] = make_float2(__uint_as_float(ld.x), __uint_as_float(ld.y));
         }
-      }
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int m0 = mtile * SBM + (wm * TM + i) * 32 + 8 * g + 4 * h;
+        for (int g = 0; g < 4; ++g) {
+          const int m0 = mtile * SBM + (wm * TM + i) * 32 + 8 * g + 4 * h;
 #pragma unroll
-        for (int py = 0; py < 2; ++py) {
-          const int k = 2 * g + py, r = 4 * g + 2 * py;  // acc rows r (px = 0), r + 1 (px = 1)
-          const float v0 = rv[k].x + acc[i][j][r] * wsc[m0 + 2 * py];
-          const float v1 = rv[k].y + acc[i][j][r + 1] * wsc[m0 + 2 * py + 1];
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(v0, v1)), rs, off[k], 0, 0);
+          for (int py = 0; py < 2; ++py) {
+            const int k = 2 * g + py, r = 4 * g + 2 * py;  // acc rows r (px = 0), r + 1 (px = 1)
+            const float v0 = rv[k].x + acc[i][j][r] * wsc[m0 + 2 * py];
+            const float v1 = rv[k].y + acc[i][j][r + 1] * wsc[m0 + 2 * py + 1];
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(v0, v1)), rs, off[k], 0, 0);
+          }
+        }
+      } else {
+        // columns x = base + 2h + px of rows y = 2jj + py: lane h = 0 holds x = base, base + 1
+        // and lane h = 1 x = base + 2, base + 3 of the same two rows; one exchange across the
+        // halves gives lane h the whole 16-B row piece of row y = 2jj + h
+        int off[4];
+        float4 rv[4];
+        const int x0 = side ? a.OW - 4 : 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = (mtile * SBM + (wm * TM + i) * 32 + 8 * g) >> 3;
+          const int y = 2 * jj + h;
+          off[g] = valid && c < a.Co ? (base + (int)(c * a.oc) + y * a.OW + x0) * 4 : a.out_bytes;
+          const u32x4 ld = __builtin_amdgcn_raw_buffer_load_b128(rs, off[g], 0, 0);
+          rv[g] = make_float4(__uint_as_float(ld.x), __uint_as_float(ld.y), __uint_as_float(ld.z),
+                              __uint_as_float(ld.w));
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int m0 = mtile * SBM + (wm * TM + i) * 32 + 8 * g + 4 * h;
+          // this lane's products: (py, px) = r & 3 at x = base + 2h + px, y = 2jj + py
+          float p00 = acc[i][j][4 * g] * wsc[m0], p01 = acc[i][j][4 * g + 1] * wsc[m0 + 1];
+          float p10 = acc[i][j][4 * g + 2] * wsc[m0 + 2], p11 = acc[i][j][4 * g + 3] * wsc[m0 + 3];
+          // send the row this lane does not store (py = 1 - h) to the partner lane (lane ^ 32)
+          const float s0 = h ? p00 : p10, s1 = h ? p01 : p11;
+          const float r0 = __shfl_xor(s0, 32), r1 = __shfl_xor(s1, 32);
+          // row y = 2jj + h: x = base .. base + 3 = (h = 0: own px 0, 1 | partner's) (h = 1: partner's | own)
+          const float k0 = h ? p10 : p00, k1 = h ? p11 : p01;
+          const float4 add = h ? make_float4(r0, r1, k0, k1) : make_float4(k0, k1, r0, r1);
+          const float4 v = make_float4(rv[g].x + add.x, rv[g].y + add.y, rv[g].z + add.z, rv[g].w + add.w);
+          __builtin_amdgcn_raw_buffer_store_b128(
+              u32x4{__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)}, rs,
+              off[g], 0, 0);
         }
       }
     }
@@ -231,10 +259,11 @@ __global__ __launch_bounds__(256) void fea_corner_kernel(FeaCornerArgs a) {
   float acc[16];
 #pragma unroll
   for (int f = 0; f < 16; ++f) acc[f] = 0.f;
-  const float* wp = a.dw + ((long)corner * 16 + p) * a.C * a.Co + c;
+  // weights [corner][ci][c][p]: a wave's 64 lanes (4 channels x 16 pixels) read 256 contiguous bytes
+  const float* wp = a.dw + ((long)corner * a.C * a.Co + c) * 16 + p;
 #pragma unroll 4
   for (int ci = 0; ci < a.C; ++ci) {
-    const float w = wp[(long)ci * a.Co];
+    const float w = wp[(long)ci * a.Co * 16];
     const float4* fv = reinterpret_cast<const float4*>(fc + ci * 16);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

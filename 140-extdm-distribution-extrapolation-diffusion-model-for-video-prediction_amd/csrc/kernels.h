@@ -207,7 +207,7 @@ bool conv_x3_phase_forward(hipStream_t s, const View& out, const View& in, const
                            float* edge = nullptr);
 // ... and its edge corrections from those lines, added into out (after the 5x5 launch):
 // side_w / side_scale the packed f16x3 line weights [pair][side][mtile][cb][tap][m32][hl][lane][8]
-// / row scales [pair][side][mt * 128], corner_w fp32 [corner][16 px][C][Co]
+// / row scales [pair][side][mt * 128], corner_w fp32 [corner][C][Co][16 px]
 struct FeaSideArgs {
   const float* e;  // edge lines [P][4][L][C]
   int C, L, T, P;

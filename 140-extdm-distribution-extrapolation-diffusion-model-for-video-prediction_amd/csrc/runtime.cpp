@@ -22,6 +22,9 @@
 
 using namespace extdm;
 
+// TrajWarp(256, tc, tp) is built with its default heads=8 (u12:805, 917), whatever attn_heads is
+static constexpr int kTrajHeads = 8;
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -603,7 +606,7 @@ struct ExtdmHandle {
     HIPCHK(hipMemcpy(fpw.side, g.data(), g.size() * sizeof(_Float16), hipMemcpyHostToDevice));
     fpw.side_scale = dmalloc(rs.size() * sizeof(float));
     HIPCHK(hipMemcpy(fpw.side_scale, rs.data(), rs.size() * sizeof(float), hipMemcpyHostToDevice));
-    // corners [corner = 2 (bottom) + (right)][p = yy * 4 + xx][ci][co]
+    // corners [corner = 2 (bottom) + (right)][ci][co][p = yy * 4 + xx]
     std::vector<float> cw((size_t)4 * 16 * Cf * Co, 0.f);
     for (int corner = 0; corner < 4; ++corner) {
       const int ky = (corner >> 1) ? n - 1 : 0, kx = (corner & 1) ? n - 1 : 0;
@@ -619,7 +622,7 @@ struct ExtdmHandle {
             double s_ = 0.0;
             for (int dy = 0; dy < 7; ++dy)
               for (int dx = 0; dx < 7; ++dx) s_ += W(co, ci, dy, dx) * dy_[dy] * dx_[dx];
-            cw[(((size_t)corner * 16 + p) * Cf + ci) * Co + co] = (float)s_;
+            cw[(((size_t)corner * Cf + ci) * Co + co) * 16 + p] = (float)s_;
           }
       }
     }
@@ -1196,14 +1199,14 @@ struct ExtdmHandle {
          ACT_RELU);
     // and split once into the cross kernel's MFMA fragments
     if (!plan && kv_split_ok())
-      REQUIRE(cross_kv_split(s, kv_k.p, kv_v.p, kvp, fea.B, fea.C, cfg.heads, cfg.tc * cfg.fea_size * cfg.fea_size),
+      REQUIRE(cross_kv_split(s, kv_k.p, kv_v.p, kvp, fea.B, fea.C, kTrajHeads, cfg.tc * cfg.fea_size * cfg.fea_size),
               "TrajWarp: k / v split not covered");
   }
   // EXTDM_CROSS_STAGED=1: the per-step kernel stages and splits K / V itself (A/B)
   bool kv_split_ok() const {
     static const bool staged = [] { const char* v = getenv("EXTDM_CROSS_STAGED"); return v && v[0] && v[0] != '0'; }();
     static const bool off = [] { const char* v = getenv("EXTDM_NO_X3_CROSS"); return v && v[0] && v[0] != '0'; }();
-    return kvp != nullptr && !staged && !off && x3_convs() && cfg.fea_ch == 32 * cfg.heads;
+    return kvp != nullptr && !staged && !off && x3_convs() && cfg.fea_ch == 32 * kTrajHeads;
   }
   // xq = maxpool(1,2,2) of the tp frames' init_noise_conv output (u12:811)
   void trajwarp_q(const View& xq, const View& fea, const View& fp_out) {
@@ -1217,10 +1220,10 @@ struct ExtdmHandle {
     if (!plan) {
       static const bool off = [] { const char* v = getenv("EXTDM_NO_X3_CROSS"); return v && v[0] && v[0] != '0'; }();
       const bool x3 = !off && x3_convs() &&
-                      (kv_split_ok() ? cross_attention_x3p(s, q.p, kvp, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs)
-                                     : cross_attention_x3(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs,
+                      (kv_split_ok() ? cross_attention_x3p(s, q.p, kvp, a.p, B, C, kTrajHeads, tp * fs * fs, tc * fs * fs)
+                                     : cross_attention_x3(s, q.p, kv_k.p, kv_v.p, a.p, B, C, kTrajHeads, tp * fs * fs,
                                                           tc * fs * fs));
-      if (!x3) cross_attention(s, q.p, kv_k.p, kv_v.p, a.p, B, C, cfg.heads, tp * fs * fs, tc * fs * fs);
+      if (!x3) cross_attention(s, q.p, kv_k.p, kv_v.p, a.p, B, C, kTrajHeads, tp * fs * fs, tc * fs * fs);
     }
     View fm2p = alloc_cf(B, C, tp, fs, fs);
     conv(fm2p, a, nullptr, P(c + ".linear_o.weight"), 1, 0, D(c + ".linear_o.bias"), nullptr, ACT_RELU);
@@ -1241,9 +1244,9 @@ struct ExtdmHandle {
     if (cfg.arch == EXTDM_ARCH_U12) {
       kv_k = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * cfg.tc * fs * fs * 4), Bm, cfg.fea_ch, cfg.tc, fs, fs);
       kv_v = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * cfg.tc * fs * fs * 4), Bm, cfg.fea_ch, cfg.tc, fs, fs);
-      if (cfg.fea_ch == 32 * cfg.heads)
+      if (cfg.fea_ch == 32 * kTrajHeads)
         kvp = reinterpret_cast<_Float16*>(
-            dmalloc(cross_kv_halves(Bm, cfg.fea_ch, cfg.heads, cfg.tc * fs * fs) * sizeof(_Float16)));
+            dmalloc(cross_kv_halves(Bm, cfg.fea_ch, kTrajHeads, cfg.tc * fs * fs) * sizeof(_Float16)));
     }
     if (cfg.arch == EXTDM_ARCH_ADA || cfg.arch == EXTDM_ARCH_ADA_U22)
       fup_all = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * T * L * L * 4), Bm, cfg.fea_ch, T, L, L);
@@ -1898,7 +1901,6 @@ struct ExtdmHandle {
     REQUIRE(cfg.dim_head == 32 || cfg.dim_head == 16, "this build supports attn_dim_head 16 or 32");
     REQUIRE(cfg.arch != EXTDM_ARCH_WO_REF || cfg.tc >= 2, "wo_ref needs at least two cond frames");
     REQUIRE(frames() <= 32, "temporal attention over more than 32 frames");
-    REQUIRE(cfg.heads % 4 == 0, "attn_heads must be a multiple of 4");
     // small tensors (biases, norm gains) go to the device now so that no
     // host->device copy can happen while a sampler step is being captured
     for (auto& kv : host)
@@ -2295,9 +2297,9 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
         fill_normal(s, fea.p, 1, (int)fea.numel(), 17, 0, 0, 4);
         fill_normal(s, q.p, 1, (int)q.numel(), 17, 0, 0, 5);
         h->trajwarp_kv(fea);
-        flop = (double)B * h->cfg.heads * 4.0 * nq * nk * (Cf / h->cfg.heads);
+        flop = (double)B * kTrajHeads * 4.0 * nq * nk * (Cf / kTrajHeads);
         launch = [&, q, a, nq, nk, Cf] {
-          REQUIRE(cross_attention_x3p(s, q.p, h->kvp, a.p, B, Cf, h->cfg.heads, nq, nk), "bench layer 8: launch rejected");
+          REQUIRE(cross_attention_x3p(s, q.p, h->kvp, a.p, B, Cf, kTrajHeads, nq, nk), "bench layer 8: launch rejected");
         };
       }
       launch();  // warm (packs the layer's weights and tables on first use)
@@ -2354,6 +2356,46 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
       return;
     }
     REQUIRE(layer != 11, "bench layer 11: the phase-composed cond_fea branch is off");
+    // layer 12: TrajWarp's linear_q, 1x1 256 -> 256 + ReLU over B x tp x fs^2 (u12:809 via
+    // MultiHeadAttentionOp, 256-row tile); layer 13: the level-2 MotionAdaptor Tmodulator, a 1x1
+    // over '(T C)' = F x C channels of B x (L/4)^2 pixels (u12:703-710, frame-major work buffers)
+    if (layer == 12 || layer == 13) {
+      std::string wn = layer == 12 ? "init_traj.cross_att.linear_q.weight" : "downs.2.4.Tmodulator.weight";
+      REQUIRE(h->has(wn), "bench layer weight missing: " + wn);
+      const PackedW& w = h->P(wn);
+      const std::string bn = wn.substr(0, wn.size() - 6) + "bias";
+      View in, out;
+      double flop = 0;
+      if (layer == 12) {
+        const int fs = h->cfg.fea_size, C = (int)h->H(wn).shape[0];
+        in = h->alloc_cf(B, C, h->cfg.tp, fs, fs);
+        out = h->alloc_cf(B, C, h->cfg.tp, fs, fs);
+        flop = 2.0 * B * h->cfg.tp * fs * fs * (double)C * C;
+      } else {
+        const int Ls = L >> 2, K = (int)h->H(wn).shape[1], M = (int)h->H(wn).shape[0];
+        in = h->alloc_tm(B, K, 1, Ls, Ls);
+        out = h->alloc_tm(B, M, 1, Ls, Ls);
+        in.st = 0; out.st = 0;
+        flop = 2.0 * B * Ls * Ls * (double)K * M;
+      }
+      fill_normal(s, in.p, 1, (int)in.numel(), 17, 0, 0, 7);
+      auto launch = [&, in, out] { h->conv(out, in, nullptr, w, 1, 0, h->D(bn), nullptr, layer == 12 ? ACT_RELU : ACT_NONE); };
+      launch();
+      hipEvent_t e0, e1;
+      HIPCHK(hipEventCreate(&e0));
+      HIPCHK(hipEventCreate(&e1));
+      HIPCHK(hipEventRecord(e0, s));
+      for (int i = 0; i < iters; ++i) launch();
+      HIPCHK(hipEventRecord(e1, s));
+      HIPCHK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      *ms_out = ms / iters;
+      *flops_out = flop;
+      return;
+    }
     static const char* names[] = {"init_conv.weight", "downs.0.0.block2.proj.weight", "downs.1.0.block2.proj.weight",
                                   "downs.2.0.block2.proj.weight", "ups.3.0.res_conv.weight",
                                   "downs.0.0.block2.proj.weight"};

@@ -240,8 +240,10 @@ class NativeWorkload:
     # `kernel`: the launched template; the PMC traffic of profiles/pmc_layer<id>.json counts
     # only when it names this template and was measured on this exact library build
     # (lib_sha16).
-    LAYERS = [(0, 'mfma', 'conv_x3_kernel<7, 1, 64, 512, 1, 8, 8, 1, true, 2, false, false, 0>',
-               'init_conv cond_fea branch 256->64 1x7x7'),
+    LAYERS = [(0, 'mfma', 'conv_x3_kernel<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true>',
+               'init_conv cond_fea branch, phase-composed: 4 phases x 64 rows, 1x5x5 over the 16x16 map, 256 ch'),
+              (11, 'mfma', 'fea_side_x3_kernel',
+               'init_conv cond_fea branch edge corrections (2 line launches K = 5 x 256, 512 rows + corners)'),
               (1, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0>',
                'level-0 ResnetBlock block1 conv 64->64 1x3x3, fp32 input staged'),
               (6, 'mfma', 'attn_x3_kernel<64, 0, 32, 8, true>',
@@ -253,7 +255,14 @@ class NativeWorkload:
               (4, 'hbm', 'conv_x3_kernel<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, false, 0>',
                'level-0 res_conv 128->64 1x1x1'),
               (9, 'mfma', 'xpath_x3_kernel<2>', 'init_conv x-branch as one composed 13x13 conv 3->64, K = 3x169'),
-              (10, 'mfma', 'noise_pool_x3_kernel', 'init_noise_conv 3->256 1x7x7 + MaxPool(1,2,2), K = 3x49')]
+              (10, 'mfma', 'noise_pool_x3_kernel', 'init_noise_conv 3->256 1x7x7 + MaxPool(1,2,2), K = 3x49'),
+              (12, 'hbm', 'conv_x3_kernel<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 0>',
+               'TrajWarp linear_q 256->256 1x1 + ReLU (256-row tile)'),
+              (13, 'mfma', 'conv_x3_kernel<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 0>',
+               'level-2 MotionAdaptor Tmodulator, 1x1 over (T C) = 3584 -> 3584 channels of 8x8 px')]
+    # HBM-bound entries: (input + output channels, spatial size per frame, frames) of the algorithmic bytes
+    HBM_BYTES = {4: lambda u, T: (128 + 64, u.latent ** 2, T),
+                 12: lambda u, T: (256 + 256, u.fea_size ** 2, u.tp)}
 
     def _traffic(self, layer, kname):
         """HBM bytes per launch from the committed PMC passes (scripts_gpu/pmc_layers.sh), only
@@ -295,8 +304,8 @@ class NativeWorkload:
                 e = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
                      'frac': round(achieved / peak, 4), 'flop_per_launch': flops}
             else:
-                cin, cout = 128, 64
-                nbytes = 4 * B * T * u.latent * u.latent * (cin + cout)
+                ch, hw, nt = self.HBM_BYTES[layer](u, T)
+                nbytes = 4 * B * nt * hw * ch
                 achieved = nbytes / (ms_layer * 1e-3) / 1e9
                 e = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'bytes_per_launch': nbytes}

@@ -460,7 +460,8 @@ def unet_forward(sd, cfg, x, time, cond_frames, cond_fea):
         if arch != 'ada_u22':
             x = F.conv3d(x, sd['init_noise_conv.weight'], sd['init_noise_conv.bias'], padding=(0, 3, 3))
         if arch == 'u12':
-            f = traj_warp(sd, 'init_traj', x[:, :, tc:], cond_fea, tc, tp, heads)
+            # TrajWarp(256, tc, tp) keeps its default heads=8 whatever attn_heads is (u12:805, 917)
+            f = traj_warp(sd, 'init_traj', x[:, :, tc:], cond_fea, tc, tp)
         else:
             f = motion_adaptor(sd, 'cond_adaptor', cond_fea, tm, tp)
             f = temporal_attention(sd, 'cond_temporal_attn', f, pb, heads, dh)
