@@ -32,14 +32,22 @@
 // [hl][c8][pos][8] (a lane's k-slice = one 16-B record, consecutive positions = consecutive
 // records: conflict-free ds_read_b128 with no swizzle, and a kx step is an immediate offset)
 // instead of [hl][pos][16] with the bit-3 swizzle
+// 1 = every one-group staged tile, 2 (default) = the k >= 5 tiles only (the 5x5 phase conv:
+// -2.5 %; the 3x3 128-row tile's LDS then no longer fits two workgroups per CU: +30 %)
 #ifndef EXTDM_X3_LIN
-#define EXTDM_X3_LIN 0
+#define EXTDM_X3_LIN 2
 #endif
 // EXTDM_X3_BUFX: the staged X loads as buffer loads (the lane's pixel offset in VGPR, the
 // channel's offset in soffset, a position outside the image past the extent so the load itself
 // returns 0): no 64-bit address VALU per load and no store-time position mask
 #ifndef EXTDM_X3_BUFX
-#define EXTDM_X3_BUFX 0
+#define EXTDM_X3_BUFX 1
+#endif
+// EXTDM_X3_EXP (diagnostic builds only, results invalid): bit 0 = the MFMAs replaced by one VALU
+// per fragment pair (operand reads kept), bit 1 = no X global loads (zeros staged), bit 2 = the
+// epilogue's output stores predicated off, bit 3 = no weight DMA
+#ifndef EXTDM_X3_EXP
+#define EXTDM_X3_EXP 0
 #endif
 
 namespace extdm {
@@ -97,6 +105,20 @@ __device__ __forceinline__ void glds16_asm(const void* gsrc, _Float16* lds) {
                : "memory");
 }
 
+// One buffer_load_dword ... lds: lane l's dword at byte offset voff of the resource lands at LDS
+// byte lds + 4 l (an offset past the resource's extent loads 0); wave-uniform LDS base in M0.
+// Asm like glds16_asm: hipcc neither waits for it nor counts it; the issuing wave's own vmcnt
+// retires it.
+__device__ __forceinline__ void bld4_asm(__amdgpu_buffer_rsrc_t rs, int voff, float* lds) {
+  const unsigned dst =
+      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rs), "s"(dst)
+               : "memory");
+}
+
 template <int KS, int BN> struct XMaxX3;
 template <> struct XMaxX3<7, 256> { static constexpr int v = 560; };
 template <> struct XMaxX3<3, 256> { static constexpr int v = 576; };
@@ -134,8 +156,18 @@ template <> struct XMaxX3<5, 256> { static constexpr int v = 400; };
 // PH: phase output (the composed fea conv, conv_x3_phase_forward): m-tile = output phase
 // (py, px) of a x2 upsampled map, row m - mtile * BM = output channel, tile pixel (row, col)
 // stored at (2 row + py, 2 col + px) of the 2H x 2W output.
+// WS: wave-specialised DMA queues. vmcnt counts one wave's memory operations in issue order,
+// so with every wave issuing both the per-stage weight DMA and the channel block's X loads, the
+// stage-end wait for the weight DMA also retired the X loads issued behind it: the X prefetch
+// had one stage (~0.6 us) to cover an L2/HBM round trip (the X loads knocked out, the 5x5 phase
+// conv ran 24 % faster, the level-0 3x3 31 %: EXTDM_X3_EXP builds). With WS the first half of
+// the waves issues only the weight DMA and waits for it at each stage end; the second half
+// issues only the X transfers (raw fp32 by buffer_load_dword ... lds into a [c][pos] tile, an
+// out-of-image position past the extent so it loads 0; or the operand by LDS-DMA) for the next
+// channel block at its first stage and waits for them at its last: STG stages of cover. The raw
+// tile is split into the [hl][c8][pos][8] operand layout by all waves between channel blocks.
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
-          bool RGN = false, int SPL = 0, bool PH = false>
+          bool RGN = false, int SPL = 0, bool PH = false, bool WS = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 && KS == 5 ? 2 : 1))) void conv_x3_kernel(X3Args a) {
   constexpr int NT = NW * 64;
   constexpr int PAD = KS / 2;
@@ -156,16 +188,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   extern __shared__ __attribute__((aligned(16))) _Float16 smx[];
   // halves from an X slot's hi block to its lo block (DMA mode: two c8 planes of whole
   // 1 KiB pieces each)
-  constexpr bool LIN = EXTDM_X3_LIN && NG == 1 && !XOP;
+  static_assert(!WS || (NG == 1 && SPAN && SPL != 2 && NW % 2 == 0), "WS: one group, spanning barriers");
+  constexpr bool WSR = WS && !XOP;  // WS with the raw fp32 tile
+  constexpr bool LIN = WSR || ((EXTDM_X3_LIN == 1 || (EXTDM_X3_LIN == 2 && KS >= 5)) && NG == 1 && !XOP);
   // halves per (hl, c8) plane: DMA mode whole 1 KiB pieces; LIN one spare position past XPOS
   // (the target of unused staging slots)
   const int XPL = ((a.XPOS + (LIN ? 1 : 0) + 63) & ~63) * 8;
   const int XLO = (XOP || LIN) ? 2 * XPL : NG * a.XPOS * 16;
   const int XH = 2 * XLO;  // halves per X slot (hi + lo)
+  constexpr int XB = WSR ? 1 : XBUF;  // WS raw: one split buffer, refilled between channel blocks
+  const int RP = (a.XPOS + 63) & ~63;  // WS raw: positions per channel row of the raw tile
   _Float16* As0 = smx;
   _Float16* As1 = smx + AHS;
   _Float16* Xs0 = smx + 2 * AHS;
-  _Float16* Xs1 = XBUF == 2 ? Xs0 + XH : Xs0;
+  _Float16* Xs1 = XB == 2 ? Xs0 + XH : Xs0;
+  float* const Xr = reinterpret_cast<float*>(Xs0 + XB * XH);  // WS raw: [16 c][RP] fp32
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -239,6 +276,13 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   const auto rsx0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in0), 0, a.in0_bytes, 0x00020000);
   const auto rsx1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in1), 0, a.in1_bytes, 0x00020000);
   auto load_x_exact = [&](int cgb) __attribute__((always_inline)) {
+#if EXTDM_X3_EXP & 2
+#pragma unroll
+    for (int j = 0; j < NSLOT; ++j)
+#pragma unroll
+      for (int c = 0; c < 16; ++c) xr[j][c] = 0.f;
+    return;
+#endif
     if (bufx) {
 #pragma unroll
       for (int j = 0; j < NSLOT; ++j) {
@@ -321,7 +365,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   // instead of branching around the store: a lane-divergent skip leaves the X loads
   // pending on one path, and hipcc's path-insensitive wait analysis then drains vmcnt(0)
   // at the next channel block's X prefetch.
-  _Float16* const xdummy = Xs0 + XBUF * XH;  // 32 halves, then the epilogue's scale/bias rows
+  _Float16* const xdummy = Xs0 + XB * XH + (WSR ? 2 * 16 * RP : 0);  // 32 halves, then the epilogue's scale/bias rows
   auto store_x = [&](_Float16* Xs, int cgb) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < NSLOT; ++j) {
@@ -371,8 +415,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   constexpr int NPIECE = AHS / 512;  // 1 KiB pieces
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   auto load_a = [&](int it, _Float16* As) {
+#if EXTDM_X3_EXP & 8
+    return;
+#endif
     const _Float16* src = wt + (long)it * AHS;
-    for (int pc = wave_u; pc < NPIECE; pc += NW) {
+    if (WS && wave_u >= NW / 2) return;  // WS: the weight waves only
+    for (int pc = wave_u; pc < NPIECE; pc += (WS ? NW / 2 : NW)) {
       if (SPAN) glds16_asm(src + pc * 512 + lane * 8, As + pc * 512);
       else
         __builtin_amdgcn_global_load_lds((const void*)(src + pc * 512 + lane * 8), (lds_ptr_t)(As + pc * 512), 16, 0,
@@ -384,10 +432,71 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   auto dma_x = [&](int cgb, _Float16* Xs) __attribute__((always_inline)) {
     const _Float16* src = a.xop + (long)cgb * a.xop_cg + (long)tb * 8;
     const int npc = (a.XPOS + 63) >> 6;  // 1 KiB pieces per plane
-    for (int pc = wave_u; pc < 4 * npc; pc += NW) {
+    if (WS && wave_u < NW / 2) return;  // WS: the X waves only
+    for (int pc = WS ? wave_u - NW / 2 : wave_u; pc < 4 * npc; pc += (WS ? NW / 2 : NW)) {
       const int pl = pc / npc, k = pc - pl * npc;  // pl = 2 * hl + c8
       glds16_asm(src + (pl >> 1) * a.xop_hl + (pl & 1) * (a.xop_hl >> 1) + k * 512 + lane * 8,
                  Xs + pl * XPL + k * 512);
+    }
+  };
+
+  // WS raw: the X waves' chunks of 64 positions of the tile (chunk k = xw + NW/2 i), each lane's
+  // position offset in both sources (bytes; past the extent when outside the image)
+  constexpr int NXW = NW / 2;
+  constexpr int WCH = WSR ? (XMaxX3<KS, BN>::v + 64 * NXW - 1) / (64 * NXW) : 1;  // chunks per X wave
+  int xo0[WCH], xo1[WCH];
+  if (WSR) {
+    const int xw = wave - NXW;
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int pos = (xw + NXW * i) * 64 + lane;
+      xo0[i] = 0x40000000; xo1[i] = 0x40000000;
+      if (xw >= 0 && pos < a.XPOS) {
+        const int p = pos / (THK * a.RS), r2 = pos - p * THK * a.RS;
+        const int rr = r2 / a.RS, cc = r2 - rr * a.RS;
+        const int q = plane0 + p, iy = row0 + rr - PAD, ix = cc - PAD;
+        if (q < a.P && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) {
+          const int b = q / a.T, t = q - b * a.T;
+          xo0[i] = (int)(((long)b * a.i0b + (long)t * a.i0t) + iy * a.W + ix) * 4;
+          xo1[i] = (int)(((long)b * a.i1b + (long)t * a.i1t) + iy * a.W + ix) * 4;
+        }
+      }
+    }
+  }
+  auto dma_raw = [&](int cgb) __attribute__((always_inline)) {
+    if (!WSR || wave_u < NXW) return;
+    const int xw = wave_u - NXW;
+#pragma unroll 4
+    for (int c = 0; c < 16; ++c) {
+      const int ci = cgb * 16 + c;  // wave-uniform; host: channel blocks never straddle the sources
+      const bool s1 = ci >= gC0;
+      const int co = (int)((s1 ? ci - gC0 : ci) * (s1 ? gi1c : gi0c)) * 4;
+#pragma unroll
+      for (int i = 0; i < WCH; ++i) {
+        const int k = xw + NXW * i;
+        if (k * 64 < a.XPOS) bld4_asm(s1 ? rsx1 : rsx0, (s1 ? xo1[i] : xo0[i]) + co, Xr + c * RP + k * 64);
+      }
+    }
+  };
+  // raw [c][pos] fp32 -> the [hl][c8][pos][8] operand layout (every wave; range flag as store_x)
+  auto split_raw = [&]() __attribute__((always_inline)) {
+    for (int p = tid; p < a.XPOS; p += NT) {
+      float v[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = Xr[c * RP + p];
+      unsigned hw[8], lw[8];
+      float am = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        split2s(v[2 * c], v[2 * c + 1], hw[c], lw[c]);
+        amax2(am, v[2 * c], v[2 * c + 1]);
+      }
+      range_bad |= am >= 65504.f;
+      _Float16* d = Xs0 + p * 8;
+      *reinterpret_cast<h8*>(d) = __builtin_bit_cast(h8, u32x4{hw[0], hw[1], hw[2], hw[3]});
+      *reinterpret_cast<h8*>(d + XPL) = __builtin_bit_cast(h8, u32x4{hw[4], hw[5], hw[6], hw[7]});
+      *reinterpret_cast<h8*>(d + 2 * XPL) = __builtin_bit_cast(h8, u32x4{lw[0], lw[1], lw[2], lw[3]});
+      *reinterpret_cast<h8*>(d + 3 * XPL) = __builtin_bit_cast(h8, u32x4{lw[4], lw[5], lw[6], lw[7]});
     }
   };
 
@@ -435,6 +544,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   } else if (XOP) {
     dma_x(c0, Xs0);
     load_a(c0 * STG, As0);
+  } else if (WSR) {
+    dma_raw(c0);
+    load_a(c0 * STG, As0);
   } else {
     load_x(c0);
     load_a(c0 * STG, As0);
@@ -443,6 +555,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   if (SPL == 2) {
   } else if (SPAN) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // the asm DMA is invisible to __syncthreads
   else __syncthreads();
+  if (WSR && SPL != 2) {
+    split_raw();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
   // One (channel block, ky block) stage. `more` = a next channel block exists (its X is
   // prefetched at stage 0 and stored at stage STG - 1). The stages of a channel block are
   // issued as stage 0 peeled + the rest, and the last channel block is peeled with
@@ -492,13 +608,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
     const int it = cgb * STG + kb;
     const int itr = it - c0 * STG, cr = cgb - c0;  // ring / buffer parity from the slice start
     const _Float16* Ast = (itr & 1) ? As1 : As0;
-    const _Float16* Xs = (cr & 1) ? Xs1 : Xs0;
+    const _Float16* Xs = (cr & 1) ? Xs1 : Xs0;  // WS raw: Xs1 == Xs0
     if (PH && !XOP && kb == 0 && a.edge && mtile == 0) export_edges(Xs, cgb);
     if (it + 1 < NIT) load_a(it + 1, (itr & 1) ? As0 : As1);
     const bool pre = (kb == 0) && more;
     if (SPAN) __builtin_amdgcn_sched_barrier(0);  // the X loads issue after the DMA (vmcnt order)
     if (pre) {
       if (XOP) dma_x(cgb + 1, (cr & 1) ? Xs0 : Xs1);
+      else if (WSR) dma_raw(cgb + 1);
       else load_x(cgb + 1);
     }
 #pragma unroll
@@ -532,12 +649,29 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
           for (int j = 0; j < TN; ++j) {
             // the scaled-lo product last: its lo_dn VALU is off the head of the chain (-3 %,
             // interleaved A/B at B = 64)
+#if EXTDM_X3_EXP & 1
+            acc[i][j][0] += (float)(al[i][0] * bh[j][0] + ah[i][1] * bh[j][1] + ad[i][2] * bl[j][2]);
+#else
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ad[i], bl[j], acc[i][j], 0, 0, 0);
+#endif
           }
       }
     }
+    }
+    if (WS) {
+      // weight waves: this stage's DMA of the next stage's slot; X waves: the next channel
+      // block's transfer at its last stage only (in flight across the other stage barriers)
+      if (wave_u < NW / 2 || (kb == STG - 1 && more))
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (WSR && kb == STG - 1 && more) {
+        split_raw();  // the split buffer's last reader (this stage) is past the barrier
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+      return;
     }
     if (!XOP && kb == STG - 1 && more) {
       if (XBUF == 1) {  // single X buffer: every wave is done with it
@@ -675,6 +809,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
         const int m = mtile * BM + (wm * TM + i) * 32 + (r16 & 3) + 8 * (r16 >> 2) + 4 * h;
         const bool ok = valid && m < a.Cout;
         const int off = ok ? (obase + (PH ? m - mtile * BM : m) * (int)a.oc) * 4 : a.out_bytes;
+#if EXTDM_X3_EXP & 4
+        if (v[r16] == 12345.678f)
+#endif
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[r16]), rs_out, off, 0, 0);
         if (do_stats) {
           const float x = ok ? v[r16] : 0.f;
@@ -726,22 +863,25 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
-          bool RGN = false, int SPL = 0, bool PH = false>
+          bool RGN = false, int SPL = 0, bool PH = false, bool WS = false>
 void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
   constexpr int AH = KY * NG * KS * (BM / 32) * 2 * 512;
-  constexpr bool LIN = EXTDM_X3_LIN && NG == 1 && !XOP;
+  constexpr bool WSR = WS && !XOP;
+  constexpr bool LIN = WSR || ((EXTDM_X3_LIN == 1 || (EXTDM_X3_LIN == 2 && KS >= 5)) && NG == 1 && !XOP);
   const size_t xlo = XOP ? (size_t)((a.XPOS + 63) & ~63) * 16
                          : (LIN ? (size_t)((a.XPOS + 1 + 63) & ~63) * 16 : (size_t)a.XPOS * NG * 16);
+  constexpr int XB = WSR ? 1 : XBUF;
+  const size_t raw = WSR ? (size_t)2 * 16 * ((a.XPOS + 63) & ~63) : 0;  // halves of the [16][RP] fp32 tile
   // + 32 halves (unused-slot dummy) + 2 * BM floats (epilogue scale / bias)
-  const size_t lds = ((size_t)2 * AH + (size_t)XBUF * 2 * xlo + 32 + 4 * BM) * sizeof(_Float16);
+  const size_t lds = ((size_t)2 * AH + (size_t)XB * 2 * xlo + raw + 32 + 4 * BM) * sizeof(_Float16);
   dim3 grid(ntiles, (a.Cout + BM - 1) / BM, SPL == 1 ? a.nsplit : 1);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH, WS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH>), grid, dim3(NW * 64), lds, s, a);
+  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH, WS>), grid, dim3(NW * 64), lds, s, a);
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN>
@@ -799,6 +939,19 @@ bool split_k(X3Args& a, unsigned ntiles, const ConvEpi& e, long max_wg, long max
   return true;
 }
 
+// EXTDM_X3_WS=<mask>: the wave-specialised staging (kernel note WS) per tile family --
+// 1 the 5x5 phase conv, 2 the staged 64-row 3x3 tile, 4 the operand-input 64-row 3x3 tile,
+// 8 the operand-input 128-row 3x3 tiles (unsplit)
+enum { kWsPhase = 1, kWsStaged64 = 2, kWsOp64 = 4, kWsOp128 = 8 };
+bool x3_ws(int fam) {
+  static const int mask = [] { const char* v = getenv("EXTDM_X3_WS"); return v ? atoi(v) : 0; }();
+  return (mask & fam) != 0;
+}
+// the raw path's preconditions: whole 16-channel blocks in each source, byte extents < 2^30
+bool x3_ws_raw_ok(const X3Args& a, int fam) {
+  return x3_ws(fam) && a.C0 % 16 == 0 && a.Cin % 16 == 0 && a.in0_bytes > 0;
+}
+
 int x3_v3() {
   static const int v3 = [] { const char* v = getenv("EXTDM_X3_V3"); return v ? atoi(v) : 0; }();
   return v3;
@@ -812,7 +965,7 @@ bool x3_w128_4(const X3Args& a, bool xop) {
   if (w == 8) return false;
   constexpr size_t AH = 3 * 4 * 2 * 512;
   const size_t xlo = xop ? (size_t)((a.XPOS + 63) & ~63) * 16
-                         : (EXTDM_X3_LIN ? (size_t)((a.XPOS + 1 + 63) & ~63) * 16 : (size_t)a.XPOS * 16);
+                         : (EXTDM_X3_LIN == 1 ? (size_t)((a.XPOS + 1 + 63) & ~63) * 16 : (size_t)a.XPOS * 16);
   return (2 * AH + 2 * 2 * xlo + 32 + 4 * 128) * sizeof(_Float16) <= 80 * 1024;
 }
 // split-K thresholds of the 3x3 128-row tile (launch_wg, total_wg): 8 waves at one workgroup
@@ -979,6 +1132,7 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     // ds_read_b128 instead of 6 per 6) at 68 KB, two independent workgroups per CU,
     // 12 % faster on the level-0 64 -> 64 conv at B = 64.
     if (x3_v3() == 1) launch<3, 3, 64, 256, 1, 4, 8, 2>(s, a, ntiles);
+    else if (x3_ws_raw_ok(a, kWsStaged64)) launch_sp<3, 1, 64, 256, 1, 4, 4, 2, true, 1, false, false, 0, false, true>(s, a, ntiles);
     else launch<3, 1, 64, 256, 1, 4, 4, 2>(s, a, ntiles);
   }
   else if (ks == 3 && tl.bm == 128) {
@@ -1050,7 +1204,8 @@ bool conv_x3_phase_forward(hipStream_t s, const View& out, const View& in, const
   if (edge && (in.H != in.W || in.C % 16 != 0 || w.xng != 1)) return false;
   a.edge = edge;
   static const int xbuf = [] { const char* v = getenv("EXTDM_FEA_XBUF"); return v ? atoi(v) : 2; }();
-  if (wt.xbn == 256) launch_sp<5, 1, 64, 256, 1, 4, 4, 1, true, 2, false, false, 0, true>(s, a, ntiles);
+  if (wt.xbn == 512 && x3_ws_raw_ok(a, kWsPhase)) launch_sp<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true, true>(s, a, ntiles);
+  else if (wt.xbn == 256) launch_sp<5, 1, 64, 256, 1, 4, 4, 1, true, 2, false, false, 0, true>(s, a, ntiles);
   else if (xbuf == 1) launch_sp<5, 1, 64, 512, 1, 8, 8, 1, true, 2, false, false, 0, true>(s, a, ntiles);
   else launch_sp<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true>(s, a, ntiles);
   return true;
@@ -1137,6 +1292,7 @@ bool conv_x3_forward_op(hipStream_t s, const View& out, const X3Op& in, const Pa
   a.xop_hl = 2 * (long)((size_t)(in.C / 16) * in.B * in.T * plane);
   if (w.xbm == 64) {
     if (x3_v3() == 1) launch_sp<3, 3, 64, 256, 1, 4, 8, 2, true, 1, true>(s, a, ntiles);
+    else if (x3_ws(kWsOp64)) launch_sp<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true, false, 0, false, true>(s, a, ntiles);
     else launch_sp<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true>(s, a, ntiles);
     return true;
   }
@@ -1150,9 +1306,11 @@ bool conv_x3_forward_op(hipStream_t s, const View& out, const X3Op& in, const Pa
     launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true, false, 1>(s, a, ntiles);
     launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true, false, 2>(s, a, ntiles);
   } else if (four) {
-    launch_sp<3, 1, 128, 128, 1, 2, 4, 2, true, 1, true>(s, a, ntiles);
+    if (x3_ws(kWsOp128)) launch_sp<3, 1, 128, 128, 1, 2, 4, 2, true, 1, true, false, 0, false, true>(s, a, ntiles);
+    else launch_sp<3, 1, 128, 128, 1, 2, 4, 2, true, 1, true>(s, a, ntiles);
   } else {
-    launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true>(s, a, ntiles);
+    if (x3_ws(kWsOp128)) launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true, false, 0, false, true>(s, a, ntiles);
+    else launch_sp<3, 1, 128, 128, 1, 2, 8, 2, true, 1, true>(s, a, ntiles);
   }
   return true;
 }
