@@ -15,7 +15,7 @@ CSRC = os.path.join(HERE, 'csrc')
 REPO = os.path.dirname(HERE)
 INCLUDE = os.path.join(REPO, 'include')
 LIB = os.path.join(HERE, 'libextdm_hip.so')
-SOURCES = ['conv.hip', 'conv_halo.hip', 'conv_x3.hip', 'conv_gemm_x3.hip', 'norm.hip', 'attn.hip', 'attn_core.hip', 'stw_fused.hip',
+SOURCES = ['conv.hip', 'conv_halo.hip', 'conv_x3.hip', 'pw_x3.hip', 'conv_gemm_x3.hip', 'norm.hip', 'attn.hip', 'attn_core.hip', 'stw_fused.hip',
            'stw_x3.hip', 'cross_x3.hip', 'xpath_x3.hip', 'fea_x3.hip', 'metrics.hip', 'sampler.hip', 'decoder.hip', 'lfae.hip', 'runtime.cpp']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-I', INCLUDE, '-I', CSRC]

@@ -237,6 +237,9 @@ void launch_bm(hipStream_t s, const ConvArgs& a, int bm, dim3 grid_n) {
 int conv_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                  int stride, int pad, const ConvEpi& epi_in) {
   int slots = 0;
+  if (w.mode == MODE_CONV && stride == 1 && w.KH == 1 && w.KW == 1 && pad == 0 && !in1 &&
+      pw_x3_forward(s, out, in0, w, epi_in))
+    return 0;
   if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 &&
       conv_x3_forward(s, out, in0, in1, w, epi_in, &slots))
     return slots;

@@ -227,6 +227,11 @@ bool fea_edges_supported(int C, int Co, int L);
 bool fea_edges_forward(hipStream_t s, const View& out, const float* edge, int C, const void* side_w,
                        const float* side_scale, const float* corner_w);
 void x3_range_reset(hipStream_t s);
+// 1x1 256 -> 256 f16x3 conv with register-resident weights (pw_x3.hip) on conv_x3's packed 1x1
+// weights (xbm 256): single input view, HW % 64 == 0, epilogue bias + ReLU only (no residual,
+// statistics or post scale). false = not covered (the caller falls back).
+// EXTDM_NO_PW=1 disables it (A/B).
+bool pw_x3_forward(hipStream_t s, const View& out, const View& in, const PackedW& w, const ConvEpi& e);
 // Evaluation metrics (metrics.hip): per-frame PSNR and SSIM in fp64.
 size_t frame_metrics_workspace(int nframes, int C, int H);
 void frame_metrics(hipStream_t s, const float* a, const float* b, int N, int T, int C, int H, int W, long sN, long sT,

@@ -256,10 +256,14 @@ class NativeWorkload:
                'level-0 res_conv 128->64 1x1x1'),
               (9, 'mfma', 'xpath_x3_kernel<2>', 'init_conv x-branch as one composed 13x13 conv 3->64, K = 3x169'),
               (10, 'mfma', 'noise_pool_x3_kernel', 'init_noise_conv 3->256 1x7x7 + MaxPool(1,2,2), K = 3x49'),
-              (12, 'hbm', 'conv_x3_kernel<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 0>',
-               'TrajWarp linear_q 256->256 1x1 + ReLU (256-row tile)'),
+              (12, 'hbm', 'pw_x3_kernel',
+               'TrajWarp linear_q 256->256 1x1 + ReLU, weights register-resident (pw_x3)'),
               (13, 'mfma', 'conv_x3_kernel<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 0>',
                'level-2 MotionAdaptor Tmodulator, 1x1 over (T C) = 3584 -> 3584 channels of 8x8 px')]
+    # Layers whose HBM reads are wide coalesced 16-B/lane streams (the operand planes by
+    # global_load_lds_dwordx4): only their PMC FETCH_SIZE gets the gfx950 x2 correction
+    # (MI355X_MICROARCH.md HBM); every other read width is reported raw (uncalibrated).
+    WIDE_READS = {5}
     # HBM-bound entries: (input + output channels, spatial size per frame, frames) of the algorithmic bytes
     HBM_BYTES = {4: lambda u, T: (128 + 64, u.latent ** 2, T),
                  12: lambda u, T: (256 + 256, u.fea_size ** 2, u.tp)}
@@ -278,7 +282,11 @@ class NativeWorkload:
             return None, 'PMC taken on another library build (stale)'
         if kname not in j.get('kernel_name', ''):
             return None, 'PMC kernel signature differs'
-        return j.get('hbm_bytes_per_launch'), 'profiles/' + os.path.basename(pmc)
+        if 'fetch_rule' not in j:
+            return None, 'PMC file predates the raw / corrected FETCH split'
+        src = (f"profiles/{os.path.basename(pmc)}: FETCH {j['fetch_bytes_raw_per_launch']} B raw, "
+               f"{j['fetch_rule']}; WRITE {j['write_bytes_per_launch']} B")
+        return j.get('hbm_bytes_per_launch'), src
 
     def roofline(self):
         """Per kernel, timed over 20 launches of the exact forward launch with HIP events

@@ -1,8 +1,11 @@
 """Per-launch HBM bytes of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE,
-WRITE_SIZE; KB units), with the gfx950 correction of MI355X_MICROARCH.md (HBM
-section): FETCH_SIZE counts half the bytes of 16-B/lane streaming reads -> x2.
-Records the launched kernel's full name and the sha256 prefix of the library the
-passes ran on, which bench.py checks before it reports the traffic."""
+WRITE_SIZE; KB units). MI355X_MICROARCH.md (HBM section): on gfx950 FETCH_SIZE counts half the
+bytes of a wide coalesced streaming read (16 B per lane) and other read widths are uncalibrated,
+so the x2 correction is applied only when the caller says the kernel's HBM reads are of that kind
+(argument `wide` = 1, bench.py WIDE_READS); otherwise hbm_bytes_per_launch is raw FETCH + WRITE.
+Both the raw FETCH and the rule used are recorded. Also records the launched kernel's full name
+and the sha256 prefix of the library the passes ran on, which bench.py checks before it reports
+the traffic. Usage: pmc_summary.py FETCH_DIR WRITE_DIR PATTERN BATCH OUT.json [wide]"""
 import csv
 import glob
 import hashlib
@@ -12,6 +15,7 @@ import re
 import sys
 
 fetch_dir, write_dir, pattern, batch, out = sys.argv[1:6]
+wide = len(sys.argv) > 6 and sys.argv[6] == '1'
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = '140-extdm-distribution-extrapolation-diffusion-model-for-video-prediction_amd'
 
@@ -62,7 +66,10 @@ res = {'kernel': pattern, 'kernel_name': names.pop(), 'batch': int(batch),
        'precision': os.environ.get('PREC', 'f16x3'), 'lib_sha16': hashlib.sha256(open(lib, 'rb').read()).hexdigest()[:16],
        'launches': [len(fe), len(wr)],
        'fetch_kb_raw_per_launch': sum(fe) / len(fe), 'write_kb_per_launch': sum(wr) / len(wr)}
-res['hbm_bytes_per_launch'] = int(2 * res['fetch_kb_raw_per_launch'] * 1024 + res['write_kb_per_launch'] * 1024)
-res['note'] = 'FETCH_SIZE doubled (gfx950 streaming-read correction); KB = 1024 B'
+res['fetch_bytes_raw_per_launch'] = int(res['fetch_kb_raw_per_launch'] * 1024)
+res['write_bytes_per_launch'] = int(res['write_kb_per_launch'] * 1024)
+res['fetch_rule'] = 'x2 (16-B/lane streaming reads, gfx950 correction)' if wide else 'raw (uncalibrated read width: no correction)'
+res['hbm_bytes_per_launch'] = int((2 if wide else 1) * res['fetch_bytes_raw_per_launch'] + res['write_bytes_per_launch'])
+res['note'] = 'KB = 1024 B; hbm = FETCH (rule above) + WRITE'
 json.dump(res, open(out, 'w'), indent=1)
 print(json.dumps(res))
