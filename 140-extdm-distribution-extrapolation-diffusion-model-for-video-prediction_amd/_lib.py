@@ -12,7 +12,7 @@ EXPORTS = ['extdm_create', 'extdm_destroy', 'extdm_last_error', 'extdm_load_weig
            'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_bench_layer',
            'extdm_decode', 'extdm_set_lfae', 'extdm_region_params', 'extdm_region_hw', 'extdm_bg_params',
            'extdm_flow_predict', 'extdm_flow_hw', 'extdm_bottleneck', 'extdm_range_flag',
-           'extdm_attn_layer', 'extdm_frame_metrics_workspace', 'extdm_frame_metrics']
+           'extdm_attn_layer', 'extdm_frame_metrics_workspace', 'extdm_frame_metrics', 'extdm_bilinear_frames']
 
 BG_TYPES = {'zero': 0, 'shift': 1, 'affine': 2, 'perspective': 3}
 
@@ -102,6 +102,9 @@ def load():
     L.extdm_frame_metrics.argtypes = [vp, vp, i32, i32, i32, i32, i32, ctypes.c_long, ctypes.c_long, ctypes.c_long,
                                       vp, vp, vp, vp]
     L.extdm_frame_metrics.restype = i32
+    lg = ctypes.c_long
+    L.extdm_bilinear_frames.argtypes = [vp, i32, i32, i32, i32, i32, vp, lg, lg, lg, vp, lg, lg, lg, i32, i32, i32, vp]
+    L.extdm_bilinear_frames.restype = i32
     _lib = L
     return L
 
@@ -113,6 +116,29 @@ def check(rc):
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def bilinear_frames(a, b, t_split, T, size):
+    """Bilinear resize (align_corners=False) into a new contiguous [B, C, T, size, size] tensor:
+    frames t < t_split from a[:, :, t], the rest from b[:, :, t - t_split] (b may have a frame
+    stride of 0, e.g. an expand()ed single frame). a / b: CUDA fp32 [B, C, t, H, W] with
+    contiguous H*W planes (extdm_bilinear_frames)."""
+    import torch
+    src = a if a is not None else b
+    Bn, C, _, H, W = src.shape
+    out = torch.empty(Bn, C, T, size[0], size[1], device=src.device, dtype=torch.float32)
+    for x in (a, b):
+        if x is not None:
+            if not x.is_cuda:
+                raise RuntimeError('ExtDM HIP path needs tensors on a ROCm device (no CPU fallback)')
+            if x.dtype != torch.float32 or x.stride(-1) != 1 or x.stride(-2) != x.shape[-1] or x.shape[-2:] != (H, W):
+                raise ValueError('bilinear_frames: fp32 [B, C, t, H, W] with contiguous planes expected')
+    sa = a.stride()[:3] if a is not None else (0, 0, 0)
+    sb = b.stride()[:3] if b is not None else (0, 0, 0)
+    with torch.cuda.device(src.device):
+        check(load().extdm_bilinear_frames(_ptr(out), Bn, C, T, size[0], size[1], _ptr(a), *sa, _ptr(b), *sb, t_split,
+                                           H, W, _stream()))
+    return out
 
 
 def _stream():

@@ -321,26 +321,25 @@ bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& 
 // init_conv's x-branch composed with init_noise_conv into 49 border-class 13x13
 // kernels (xpath_x3.hip): out[:, :Cout] = sum_c K_c * x + cbias_c for the 3-channel x
 struct XPathArgs {
-  const float* x; long xb, xc, xt;  // the zero-padded copy (xpad_forward)
+  const float* x; long xb, xc, xt;  // the zero-padded pre-split copy (xpad_forward; dwords)
   int T, L, F, LP;
   float* out; long ob, oc, ot; int Cout;
   const _Float16* w; const float* rscale; const float* cbias;
-  int* range;
   int tile_start[50];
 };
 bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
                       const float* cbias);
 // the zero-padded copy of the 3-channel x both kernels above read: [B][3][T][LP][LP], x at
-// (6, 6), LP = xpad_size(L)
+// (6, 6), LP = xpad_size(L), one dword per position holding its f16x3 pair (hi | lo' << 16,
+// lo' = fp16((v - hi) 2^11)); the range flag (|v| >= 65504) is raised here
 int xpad_size(int L);
 void xpad_forward(hipStream_t s, const View& xpad, const View& x);
 // maxpool(1,2,2)(init_noise_conv(x)) in one kernel (xpath_x3.hip): out [B][C][T][L/2][L/2]
 struct NoisePoolArgs {
-  const float* x; long xb, xc, xt;  // the zero-padded copy (xpad_forward)
+  const float* x; long xb, xc, xt;  // the zero-padded pre-split copy (xpad_forward; dwords)
   int T, L, F, LP;
   float* out; long ob, oc, ot; int Cout;
   const _Float16* w; const float* rscale; const float* bias;
-  int* range;
 };
 bool noise_pool_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
                            const float* bias);

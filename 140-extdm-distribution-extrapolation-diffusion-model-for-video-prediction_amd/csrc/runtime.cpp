@@ -2038,6 +2038,25 @@ int extdm_frame_metrics(const float* a, const float* b, int N, int T, int C, int
   });
 }
 
+int extdm_bilinear_frames(float* dst, int B, int C, int T, int OH, int OW, const float* a, long a_sb, long a_sc,
+                          long a_st, const float* b, long b_sb, long b_sc, long b_st, int t_split, int H, int W,
+                          void* stream) {
+  return guarded([&] {
+    REQUIRE(dst && (a || t_split == 0) && (b || t_split >= T), "bilinear_frames: null pointer");
+    REQUIRE(B > 0 && C > 0 && T > 0 && OH > 0 && OW > 0 && H > 0 && W > 0 && t_split >= 0 && t_split <= T,
+            "bilinear_frames: bad geometry");
+    View d = cf_view(dst, B, C, T, OH, OW);
+    View va = cf_view(const_cast<float*>(a ? a : b), B, C, T, H, W);
+    va.sb = a_sb; va.sc = a_sc; va.st = a_st;
+    View vb = cf_view(const_cast<float*>(b ? b : a), B, C, T, H, W);
+    vb.sb = b_sb; vb.sc = b_sc; vb.st = b_st;
+    if (!a) va = vb;
+    if (!b) vb = va;
+    bilinear_frames(reinterpret_cast<hipStream_t>(stream), d, va, vb, t_split);
+    HIPCHK(hipGetLastError());
+  });
+}
+
 int extdm_create(const ExtdmConfig* cfg, ExtdmHandle** out) {
   return guarded([&] {
     REQUIRE(cfg && out, "null argument");

@@ -19,8 +19,8 @@
 // 16 columns (13 used), N = the class's pixels over all frames (a class's pixel set
 // is rows(cy) x cols(cx) of every frame). One wave owns 64 pixels (two n32 tiles) and
 // all output channels; A (the class's packed weights, [kstep][m32][hl][lane][8]) is
-// read straight from L2, B is gathered from x (8 consecutive columns per lane and
-// k-step) and split into hi / lo in registers. No LDS, no barriers.
+// read straight from L2, B is gathered from the pre-split copy of x (8 consecutive columns per
+// lane and k-step, already hi / lo'). No LDS, no barriers.
 #include "kernels.h"
 
 namespace extdm {
@@ -36,40 +36,40 @@ __device__ __forceinline__ f32x16 mma3(const h8& ah, const h8& al, const h8& bh,
   // the scaled-lo product last, so its lo_dn VALU is off the head of the chain
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(lo_dn(ah), bl, c, 0, 0, 0);  // scaled x lo (gather8p)
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(lo_dn(ah), bl, c, 0, 0, 0);  // scaled x lo (xpad_kernel)
   return c;
 }
 
-// hi / lo' fragments of 8 consecutive values of a row of the zero-padded copy of x (xpad_kernel):
-// two 16-B loads (dword alignment suffices for global_load_dwordx4) and no per-element index,
-// clamp or mask VALU (the round-2 gather8 spent ~10 VALU per value on them: 158 VALU per 12
-// MFMAs in xpath's k-loop). Columns the composed kernels do not use (dx >= 13, noise_pool's
-// 8th column) are read from the padding or the next columns and meet zero weights: the
-// values are finite, so their products are exact zeros. Compiler-visible split (the
-// fragments feed MFMAs directly; kernels.h split2 note), lo scaled by 2^11 (split2s).
-__device__ __forceinline__ void gather8p(const float* p, h8& bh, h8& bl, float& am) {
-  const float4 u = *reinterpret_cast<const float4*>(p);
-  const float4 w = *reinterpret_cast<const float4*>(p + 4);
-  const float v[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
-  // lo' = fp16(fma(hi, -2^11, 2^11 v)): v * 2^11 exact, the fma exact (hi agrees with v in
-  // its leading 11 bits), one rounding; hi enters the v_fma_mix as its fp16 register
-  const float up = split_src(X3_LO_UP);
+// hi / lo' fragments of 8 consecutive positions of a row of the zero-padded, pre-split copy of x
+// (xpad_kernel: one dword per position, hi in the low half, lo' = fp16((v - hi) 2^11) in the
+// high half): two 16-B loads (dword alignment suffices for global_load_dwordx4) and 8 v_perm_b32,
+// no index, clamp, mask or split VALU in the k-loop (the round-3 fp32 copy split every gathered
+// value again in each of the 13 k-steps that read it: 8.8 VALU per MFMA in xpath's k-loop,
+// profiles/r04_sq_layers.txt). Columns the composed kernels do not use (dx >= 13, noise_pool's
+// 8th column) are read from the padding or the next columns and meet zero weights: the values
+// are finite, so their products are exact zeros.
+__device__ __forceinline__ void gather8p(const unsigned* p, h8& bh, h8& bl) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint4 w = *reinterpret_cast<const uint4*>(p + 4);
+  const unsigned v[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+  unsigned hi[4], lo[4];
 #pragma unroll
-  for (int e = 0; e < 8; e += 2) {
-    const float v0 = split_src(v[e]), v1 = split_src(v[e + 1]);
-    amax2(am, v0, v1);  // loaded values, not MFMA results: the asm form is hazard-free here
-    const f16x2_t hh = __builtin_convertvector((f32x2_t){v0, v1}, f16x2_t);
-    bh[e] = hh.x; bh[e + 1] = hh.y;
-    bl[e] = (_Float16)__builtin_fmaf((float)hh.x, -up, v0 * up);
-    bl[e + 1] = (_Float16)__builtin_fmaf((float)hh.y, -up, v1 * up);
+  for (int e = 0; e < 4; ++e) {
+    hi[e] = __builtin_amdgcn_perm(v[2 * e + 1], v[2 * e], 0x05040100u);  // low halves
+    lo[e] = __builtin_amdgcn_perm(v[2 * e + 1], v[2 * e], 0x07060302u);  // high halves
   }
+  bh = __builtin_bit_cast(h8, u32x4{hi[0], hi[1], hi[2], hi[3]});
+  bl = __builtin_bit_cast(h8, u32x4{lo[0], lo[1], lo[2], lo[3]});
 }
 
 // x [B][3][T][L][L] -> xpad [B][3][T][LP][LP] with x at (6, 6) and zeros around (LP >= L + 16:
 // xpath reads rows py - 6 .. py + 6 and columns px - 6 .. px + 9, noise_pool rows 2yp - 3 ..
-// 2yp + 5 and columns lc - 3 .. lc + 4)
+// 2yp + 5 and columns lc - 3 .. lc + 4), each position split once into the f16x3 pair
+// (hi | lo' << 16; lo' = fp16(fma(hi, -2^11, 2^11 v)): v * 2^11 exact, the fma exact, one
+// rounding) and range-checked here for both consumers
 __global__ __launch_bounds__(256) void xpad_kernel(const float* __restrict__ x, long xb, long xc, long xt,
-                                                   float* __restrict__ xp, int T, int L, int LP, long n) {
+                                                   unsigned* __restrict__ xp, int T, int L, int LP, long n,
+                                                   int* range) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const int col = (int)(i % LP), row = (int)((i / LP) % LP);
@@ -77,7 +77,12 @@ __global__ __launch_bounds__(256) void xpad_kernel(const float* __restrict__ x, 
   const int t = (int)(pl % T), ci = (int)((pl / T) % 3);
   const long b = pl / (3L * T);
   const int y = row - 6, xx = col - 6;
-  xp[i] = (y >= 0 && y < L && xx >= 0 && xx < L) ? x[b * xb + ci * xc + t * xt + (long)y * L + xx] : 0.f;
+  const float v = split_src((y >= 0 && y < L && xx >= 0 && xx < L) ? x[b * xb + ci * xc + t * xt + (long)y * L + xx] : 0.f);
+  if (fabsf(v) >= 65504.f) atomicOr(range, 1);
+  const _Float16 hi = (_Float16)v;
+  const float up = split_src(X3_LO_UP);
+  const _Float16 lo = (_Float16)__builtin_fmaf((float)hi, -up, v * up);
+  xp[i] = (unsigned)__builtin_bit_cast(unsigned short, hi) | ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16);
 }
 
 __device__ __forceinline__ void class_span(int c, int L, int& start, int& count) {
@@ -127,9 +132,9 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
       for (int r = 0; r < 16; ++r) acc[m][nt][r] = 0.f;
 
   const _Float16* wc = a.w + (long)cls * KSTEPS * M32 * 1024 + lane * 8;
-  float am = 0.f;
+  const unsigned* const xu = reinterpret_cast<const unsigned*>(a.x);
   for (int ci = 0; ci < 3; ++ci) {
-    const float* xc = a.x + (long)ci * a.xc + 8 * h;
+    const unsigned* xc = xu + (long)ci * a.xc + 8 * h;
     // whole rows unrolled: the next k-steps' x / weight loads issue ahead of this one's MFMAs
 #pragma unroll
     for (int dy = 0; dy < 13; ++dy) {
@@ -143,15 +148,13 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
       }
       h8 bh[2], bl[2];
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) gather8p(xc + xoff[nt] + dy * a.LP, bh[nt], bl[nt], am);
+      for (int nt = 0; nt < 2; ++nt) gather8p(xc + xoff[nt] + dy * a.LP, bh[nt], bl[nt]);
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
         for (int m = 0; m < M32; ++m) acc[m][nt] = mma3(ah[m], al[m], bh[nt], bl[nt], acc[m][nt]);
     }
   }
-  if (am >= 65504.f) atomicOr(a.range, 1);
-
   // ---- epilogue (C/D map: col = lane & 31, row = (r&3) + 8(r>>2) + 4h) ----
   const float* rs = a.rscale + (long)cls * M32 * 32;
   const float* cb = a.cbias + (long)cls * M32 * 32;
@@ -191,7 +194,8 @@ __global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
   const int b = f / a.T, t = f - b * a.T;
   const bool ok = lc < L;
   // padded copy: row 2yp + nt + dy + 3, column lc + 3 (+ e)
-  const float* xf = a.x + (long)b * a.xb + (long)t * a.xt + (long)(2 * yp + 3) * a.LP + (ok ? lc : 0) + 3;
+  const unsigned* xf =
+      reinterpret_cast<const unsigned*>(a.x) + (long)b * a.xb + (long)t * a.xt + (long)(2 * yp + 3) * a.LP + (ok ? lc : 0) + 3;
 
   f32x16 acc[MW][2];
 #pragma unroll
@@ -202,7 +206,6 @@ __global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
       for (int r = 0; r < 16; ++r) acc[m][nt][r] = 0.f;
   const _Float16* wq = a.w + (long)mq * MW * 1024 + lane * 8;
   const int M32 = (a.Cout + 31) / 32;
-  float am = 0.f;
 #pragma unroll 2
   for (int ks = 0; ks < 12; ++ks) {
     const int ci = ks / 4, dy = 2 * (ks % 4) + h;
@@ -215,13 +218,12 @@ __global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
     }
     h8 bh[2], bl[2];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) gather8p(xf + (long)ci * a.xc + (nt + dy) * a.LP, bh[nt], bl[nt], am);
+    for (int nt = 0; nt < 2; ++nt) gather8p(xf + (long)ci * a.xc + (nt + dy) * a.LP, bh[nt], bl[nt]);
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int m = 0; m < MW; ++m) acc[m][nt] = mma3(ah[m], al[m], bh[nt], bl[nt], acc[m][nt]);
   }
-  if (am >= 65504.f) atomicOr(a.range, 1);
   float* of = a.out + (long)b * a.ob + (long)t * a.ot + (long)yp * Lh + (lc >> 1);
 #pragma unroll
   for (int m = 0; m < MW; ++m)
@@ -240,8 +242,8 @@ int xpad_size(int L) { return (L + 16 + 7) & ~7; }
 
 void xpad_forward(hipStream_t s, const View& xpad, const View& x) {
   const long n = (long)x.B * 3 * x.T * xpad.H * xpad.W;
-  hipLaunchKernelGGL(xpad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x.p, x.sb, x.sc, x.st, xpad.p, x.T,
-                     x.H, xpad.W, n);
+  hipLaunchKernelGGL(xpad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x.p, x.sb, x.sc, x.st,
+                     reinterpret_cast<unsigned*>(xpad.p), x.T, x.H, xpad.W, n, x3_range_ptr());
 }
 
 // x: the zero-padded copy (xpad_forward; LP = x.W, the latent L = out.H * 2)
@@ -255,7 +257,7 @@ bool noise_pool_x3_forward(hipStream_t s, const View& out, const View& x, const 
   a.x = x.p; a.xb = x.sb; a.xc = x.sc; a.xt = x.st; a.LP = x.W;
   a.T = x.T; a.L = L; a.F = x.B * x.T;
   a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
-  a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.bias = bias; a.range = x3_range_ptr();
+  a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.bias = bias;
   const long units = (long)a.F * (L / 2) * ((out.C + 32 * NP_MW - 1) / (32 * NP_MW));
   hipLaunchKernelGGL(noise_pool_x3_kernel, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, s, a);
   return true;
@@ -272,7 +274,7 @@ bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void*
   a.x = x.p; a.xb = x.sb; a.xc = x.sc; a.xt = x.st; a.LP = x.W;
   a.T = x.T; a.L = L; a.F = x.B * x.T;
   a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
-  a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.cbias = cbias; a.range = x3_range_ptr();
+  a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.cbias = cbias;
   a.tile_start[0] = 0;
   for (int c = 0; c < 49; ++c) {
     const int cy = c / 7, cx = c % 7;

@@ -304,14 +304,13 @@ class FlowDiffusion(nn.Module):
         early = self.generator.forward_bottle(frames[:(tc - 1) * B]) if tc > 1 else ref_fea[:0]
         early = early.reshape(tc - 1, B, *ref_fea.shape[1:])
         if self.wrapper == 'multi1248':
-            # ... x tp, bilinear to the flow size (multi1248.py:240-245)
-            feas = [early[i] for i in range(tc - 1)] + [ref_fea] * tp
-            fea = torch.stack(feas, dim=2)
-            n, c, t, hh, ww = fea.shape
+            # ... x tp, bilinear to the flow size (multi1248.py:240-245), on the HIP library: the
+            # tc - 1 early maps and ONE resize of the repeated reference map per output frame
+            # (a frame stride of 0), written straight into the [B, C, tc - 1 + tp, fs, fs] tensor
             fs = ret['real_vid_grid'].shape[-1]
-            fea = torch.nn.functional.interpolate(fea.permute(0, 2, 1, 3, 4).reshape(n * t, c, hh, ww),
-                                                  size=(fs, fs), mode='bilinear')
-            fea = fea.reshape(n, t, c, fs, fs).permute(0, 2, 1, 3, 4)
+            early_t = early.permute(1, 2, 0, 3, 4)  # [B, C, tc - 1, h, w]
+            fea = _lib.bilinear_frames(early_t if tc > 1 else None, ref_fea.unsqueeze(2).expand(-1, -1, tp, -1, -1),
+                                       tc - 1, tc - 1 + tp, (fs, fs))
         else:
             feas = [early[i] for i in range(tc - 1)] + [ref_fea] * (1 + tp)
             fea = torch.stack(feas, dim=2)

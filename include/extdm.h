@@ -198,6 +198,15 @@ size_t extdm_frame_metrics_workspace(int N, int T, int C, int H, int W);
 int extdm_frame_metrics(const float* a, const float* b, int N, int T, int C, int H, int W, long sN, long sT, long sC,
                         double* psnr, double* ssim, void* work, void* stream);
 
+/* Bilinear resize (align_corners=False, F.interpolate(mode='bilinear')) of frames into a
+ * contiguous dst [B][C][T][OH][OW]: frame t < t_split from a at frame t, frame t >= t_split from
+ * b at frame t - t_split (element strides per batch / channel / frame; planes contiguous H*W;
+ * a frame stride of 0 repeats one frame). Replaces the multi1248 wrapper's per-frame
+ * interpolate of the cond features (multi1248.py:240-245). Not tied to a handle. */
+int extdm_bilinear_frames(float* dst, int B, int C, int T, int OH, int OW, const float* a, long a_sb, long a_sc,
+                          long a_st, const float* b, long b_sb, long b_sc, long b_st, int t_split, int H, int W,
+                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

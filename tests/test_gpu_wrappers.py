@@ -115,3 +115,24 @@ def test_ddpm100_chain_vs_reference():
     torch.cuda.synchronize()
     err = np.abs(out.cpu().numpy() - g['ddpm100']).max()
     assert err <= 5e-4, err
+
+
+def test_bilinear_frames_matches_interpolate():
+    """extdm_bilinear_frames (the multi1248 wrapper's cond-feature resize, multi1248.py:240-245)
+    against F.interpolate(mode='bilinear') on the CPU: early frames from one tensor, a repeated
+    reference frame through a frame stride of 0."""
+    import torch.nn.functional as F
+    from tests.golden_inputs import PKG
+    import importlib
+    lib = importlib.import_module(PKG)._lib
+    g = torch.Generator().manual_seed(7)
+    B, C, te, tp, h, fs = 2, 5, 3, 4, 8, 32
+    early = torch.randn(B, C, te, h, h, generator=g)
+    ref = torch.randn(B, C, h, h, generator=g)
+    out = lib.bilinear_frames(early.cuda(), ref.cuda().unsqueeze(2).expand(-1, -1, tp, -1, -1), te, te + tp,
+                              (fs, fs)).cpu()
+    full = torch.cat([early, ref.unsqueeze(2).expand(-1, -1, tp, -1, -1)], dim=2)
+    want = F.interpolate(full.permute(0, 2, 1, 3, 4).reshape(-1, C, h, h), size=(fs, fs), mode='bilinear')
+    want = want.reshape(B, te + tp, C, fs, fs).permute(0, 2, 1, 3, 4)
+    assert out.shape == want.shape
+    assert (out - want).abs().max().item() <= 1e-6
