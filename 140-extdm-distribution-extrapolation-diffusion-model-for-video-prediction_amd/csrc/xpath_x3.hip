@@ -23,6 +23,11 @@
 // lane and k-step, already hi / lo'). No LDS, no barriers.
 #include "kernels.h"
 
+// EXTDM_XP_EXP (diagnostic builds only, results invalid): bit 0 = xpath's output stores predicated off
+#ifndef EXTDM_XP_EXP
+#define EXTDM_XP_EXP 0
+#endif
+
 namespace extdm {
 
 namespace {
@@ -166,6 +171,9 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+#if EXTDM_XP_EXP & 1
+        if (acc[m][nt][r] == 12345.678f)
+#endif
         if (row < a.Cout) a.out[ooff[nt] + (long)row * a.oc] = acc[m][nt][r] * rs[row] + cb[row];
       }
   }
