@@ -247,25 +247,25 @@ class NativeWorkload:
     # `kernel`: the launched template; the PMC traffic of profiles/pmc_layer<id>.json counts
     # only when it names this template and was measured on this exact library build
     # (lib_sha16).
-    LAYERS = [(0, 'mfma', 'conv_x3_kernel<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true>',
+    LAYERS = [(0, 'mfma', 'conv_x3_kernel<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true, false>',
                'init_conv cond_fea branch, phase-composed: 4 phases x 64 rows, 1x5x5 over the 16x16 map, 256 ch'),
               (11, 'mfma', 'fea_side_x3_kernel',
                'init_conv cond_fea branch edge corrections (2 line launches K = 5 x 256, 512 rows + corners)'),
-              (1, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0>',
+              (1, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0, false, false>',
                'level-0 ResnetBlock block1 conv 64->64 1x3x3, fp32 input staged'),
               (6, 'mfma', 'attn_x3_kernel<64, 0, 32, 8, true>',
                'level-0 shifted-window attention (STW, C 64, 2x4x4 windows, 8 heads x 32), fused LN/qkv/proj'),
-              (5, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true, false, 0>',
+              (5, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true, false, 0, false, false>',
                'level-0 ResnetBlock block2 conv 64->64 1x3x3, pre-split operand by LDS-DMA'),
               (7, 'mfma', 'attn_x3_kernel<64, 1, 32, 8, true>', 'init_temporal_attn (C 64, 16 frames, 8 heads x 32), x tile by LDS-DMA'),
               (8, 'mfma', 'cross_attn_x3p_kernel<1>', 'TrajWarp cross-attention core (3584 queries x 512 keys, 8 heads)'),
-              (4, 'hbm', 'conv_x3_kernel<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, false, 0>',
+              (4, 'hbm', 'conv_x3_kernel<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, false, 0, false, false>',
                'level-0 res_conv 128->64 1x1x1'),
               (9, 'mfma', 'xpath_x3_kernel<2>', 'init_conv x-branch as one composed 13x13 conv 3->64, K = 3x169'),
               (10, 'mfma', 'noise_pool_x3_kernel', 'init_noise_conv 3->256 1x7x7 + MaxPool(1,2,2), K = 3x49'),
               (12, 'hbm', 'pw_x3_kernel',
                'TrajWarp linear_q 256->256 1x1 + ReLU, weights register-resident (pw_x3)'),
-              (13, 'mfma', 'conv_x3_kernel<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 0>',
+              (13, 'mfma', 'conv_x3_kernel<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 0, false, false>',
                'level-2 MotionAdaptor Tmodulator, 1x1 over (T C) = 3584 -> 3584 channels of 8x8 px')]
     # Layers whose HBM reads are wide coalesced 16-B/lane streams (the operand planes by
     # global_load_lds_dwordx4): only their PMC FETCH_SIZE gets the gfx950 x2 correction
