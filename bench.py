@@ -267,10 +267,14 @@ class NativeWorkload:
                'TrajWarp linear_q 256->256 1x1 + ReLU, weights register-resident (pw_x3)'),
               (13, 'mfma', 'conv_x3_kernel<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 0, false, false>',
                'level-2 MotionAdaptor Tmodulator, 1x1 over (T C) = 3584 -> 3584 channels of 8x8 px')]
-    # Layers whose HBM reads are wide coalesced 16-B/lane streams (the operand planes by
-    # global_load_lds_dwordx4): only their PMC FETCH_SIZE gets the gfx950 x2 correction
-    # (MI355X_MICROARCH.md HBM); every other read width is reported raw (uncalibrated).
-    WIDE_READS = {5}
+    # Layers whose HBM reads are whole-line coalesced streams (every wave instruction reads >= 256
+    # contiguous bytes: buffer loads of 64 consecutive pixels, 1-KB LDS-DMA pieces): their PMC
+    # FETCH_SIZE gets the gfx950 x2 correction (MI355X_MICROARCH.md HBM), calibrated here on
+    # pw_x3 (layer 12), which reads each of its 234.9 MB of input exactly once: raw FETCH 118.8 MB
+    # (0.506x). Not doubled (reported raw, uncalibrated): the x-branch gathers (9, 10: overlapping
+    # per-lane 32-B windows) and the temporal attention (7: 16-B pieces four pixels wide, one
+    # frame apart; raw 287.6 MB against 268 MB of x).
+    WIDE_READS = {0, 1, 4, 5, 6, 8, 11, 12, 13}
     # HBM-bound entries: (input + output channels, spatial size per frame, frames) of the algorithmic bytes
     HBM_BYTES = {4: lambda u, T: (128 + 64, u.latent ** 2, T),
                  12: lambda u, T: (256 + 256, u.fea_size ** 2, u.tp)}
@@ -443,6 +447,7 @@ def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
         t0 = time.perf_counter()
         ret, x_cond, fea, ref = LO.encode_round(sd, lc, ucfg, vid)
         t_enc = time.perf_counter() - t0
+        print(f'cpu baseline: encoder round {t_enc:.2f} s', file=sys.stderr, flush=True)
         if fd.wrapper == 'multi1248':  # cond_fea at flow size, tc - 1 + tp frames (multi1248.py:240-245)
             fea = torch.randn(1, fea.shape[1], ucfg.tc - 1 + ucfg.tp, ucfg.latent, ucfg.latent)
         x = torch.randn(1, 3, ucfg.tp, ucfg.latent, ucfg.latent)
@@ -473,6 +478,9 @@ def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
                 t0 = time.perf_counter()
                 xb = step(k + 1, xb)
                 per.append(time.perf_counter() - t0)
+                # progress on stderr (stdout carries the one JSON line)
+                print(f'cpu baseline: {nth} threads, B={B}: step {k + 1}/{n_steps} {per[-1]:.2f} s', file=sys.stderr,
+                      flush=True)
             t_step = float(np.median(per))
             total = rounds * B * (t_enc + t_dec) + rounds * steps_per_round * t_step
             points.append({'threads': nth, 'batch': B, 'frames_per_s': round(rounds * ucfg.tp * B / total, 5),

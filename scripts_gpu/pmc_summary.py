@@ -68,7 +68,8 @@ res = {'kernel': pattern, 'kernel_name': names.pop(), 'batch': int(batch),
        'fetch_kb_raw_per_launch': sum(fe) / len(fe), 'write_kb_per_launch': sum(wr) / len(wr)}
 res['fetch_bytes_raw_per_launch'] = int(res['fetch_kb_raw_per_launch'] * 1024)
 res['write_bytes_per_launch'] = int(res['write_kb_per_launch'] * 1024)
-res['fetch_rule'] = 'x2 (16-B/lane streaming reads, gfx950 correction)' if wide else 'raw (uncalibrated read width: no correction)'
+res['fetch_rule'] = ('x2 (whole-line streaming reads, gfx950 correction; calibrated on pw_x3: 0.506x)' if wide
+                     else 'raw (uncalibrated read pattern: no correction)')
 res['hbm_bytes_per_launch'] = int((2 if wide else 1) * res['fetch_bytes_raw_per_launch'] + res['write_bytes_per_launch'])
 res['note'] = 'KB = 1024 B; hbm = FETCH (rule above) + WRITE'
 json.dump(res, open(out, 'w'), indent=1)
