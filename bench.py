@@ -411,13 +411,35 @@ def cpu_model():
     return 'unknown'
 
 
+def cgroup_cpus():
+    """CPUs' worth of time the cgroup grants this process (cpu.max quota / period; cgroup v1
+    cfs quota), or None when unlimited / unknown."""
+    try:
+        q, p = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            return max(1, math.ceil(int(q) / int(p)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+        p = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+        return max(1, math.ceil(q / p)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_threads():
-    """Host cores this process may run on (sched affinity), and the OMP_NUM_THREADS slice
-    where one is set (the GPU box's per-GPU CPU share; else all cores)."""
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    """Host cores this process may run on (sched affinity, capped by the cgroup CPU quota: on
+    the GPU box 256 cores are visible but the container is granted a 16-CPU share, and 256
+    threads on it took 87 s for the oracle's encoder round), and the OMP_NUM_THREADS slice
+    where one is set. Returns (visible cores, usable cores, slice)."""
+    visible = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    quota = cgroup_cpus()
+    usable = min(visible, quota) if quota else visible
     env = os.environ.get('OMP_NUM_THREADS')
-    threads = min(cores, int(env)) if env and env.isdigit() and int(env) > 0 else cores
-    return cores, threads
+    threads = min(usable, int(env)) if env and env.isdigit() and int(env) > 0 else usable
+    return visible, usable, threads
 
 
 def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
@@ -430,7 +452,7 @@ def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
     that slice (reported beside it, not the value). Oracle use is confined to this untimed leg."""
     from oracle import extdm_oracle as O
     from oracle import lfae_oracle as LO
-    cores, slice_threads = cpu_threads()
+    visible, cores, slice_threads = cpu_threads()
     threads = cores
     torch.set_num_threads(threads)
     ucfg = fd.unet.ucfg
@@ -489,9 +511,12 @@ def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
     best = max((p for p in points if p['threads'] == threads), key=lambda p: p['frames_per_s'])
     return {'value': best['frames_per_s'], 'unit': 'frames/s', 'cores': cores, 'threads': threads,
             'kind': 'port', 'cpu_model': cpu_model(), 'batch_points': points,
-            'baseline_method': 'r04: all host cores (value) + the OMP_NUM_THREADS slice at B=1; median of '
+            'visible_cores': visible, 'cgroup_cpus': cgroup_cpus(),
+            'baseline_method': 'r04: every host core the process may use (sched affinity capped by the cgroup '
+                               'CPU quota; value) + the OMP_NUM_THREADS slice at B=1 where smaller; median of '
                                f'{n_steps} timed steps per point (r03: the OMP slice only, 3 steps)',
-            'sample': f'oracle (PyTorch-CPU fp32) on {threads} threads = all {cores} host cores: encoder round '
+            'sample': f'oracle (PyTorch-CPU fp32) on {threads} threads = every usable host core ({visible} '
+                      f'visible, cgroup quota {cgroup_cpus()}): encoder round '
                       f'({t_enc:.3f} s) and decode round ({t_dec:.3f} s) at B=1, {n_steps} '
                       f'{"DDIM" if ddim else "DDPM"} steps per batch point (B = '
                       f'{", ".join(str(p["batch"]) for p in points if p["threads"] == threads)}'
