@@ -195,7 +195,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   // Operand scales. An fp16 lo below 2^-14 is subnormal, so a split operand far below unit
   // scale loses bits (tests/test_gpu_precision.py activation-scale cases); here every split
   // operand is brought near unit scale by powers of two (exact): the normalised input by
-  // 2^e_w, e_w from the workgroup's largest |value| (prologue), and wsc (packed_attn_x3,
+  // 2^e_w, e_w from the wave's (tile paths: the workgroup's) largest |value| (prologue), and wsc (packed_attn_x3,
   // runtime.cpp) takes the MFMA results (weights pre-scaled per matrix) to q * q_scale *
   // 2^e_q, k * 2^e_k, v * 2^e_v once 2^-e_w is folded in, exponents estimated from the
   // weights and the norm's affine for an input of unit largest value;
@@ -411,9 +411,15 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
           xv[k][e] = ((xv[k][e] - m2) * rstd2 * (T1 ? parL[64 + 16 * k + 8 * h + e] : ldb(rs_lw, 32 * h, (16 * k + e) * 4)) +
                       (T1 ? parL[128 + 16 * k + 8 * h + e] : ldb(rs_lb, 32 * h, (16 * k + e) * 4))) * vm;
     }
-    // e_w: the workgroup's largest |normalised value| to [2^8, 2^9) (a LayerNorm whose variance
-    // is below its eps leaves the output far from unit scale, so this is data-dependent);
-    // one barrier, which also retires every wave's tile reads before PIPE reuses the tile
+    // e_w: the largest |normalised value| to [2^8, 2^9) (a LayerNorm whose variance is below
+    // its eps leaves the output far from unit scale, so this is data-dependent). On the tile
+    // paths it is the workgroup's (wave 0 folds the q / k scales into the RoPE factors every
+    // wave reads from LDS; a tile workgroup is one window row / pixel run of one sample); on the
+    // per-lane path it is the wave's own: a wave owns one window or pixel set of one sample,
+    // whereas that workgroup spans two samples when the groups per sample are not a multiple
+    // of NW, and a sample's lo roundings must not depend on its batch neighbour (bitwise batch
+    // independence). One barrier, which also retires every wave's tile reads before PIPE reuses
+    // the tile.
     float am = 0.f;
 #pragma unroll
     for (int k = 0; k < KS; ++k)
@@ -424,9 +430,12 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     for (int off = 1; off < 32; off <<= 1) am = fmaxf(am, __shfl_xor(am, off));
     if (lane == 0) redL[wave] = am;
     __syncthreads();
-    float wm = redL[0];
+    float wm = am;
+    if (TILE || PIPE) {
+      wm = redL[0];
 #pragma unroll
-    for (int i = 1; i < NW; ++i) wm = fmaxf(wm, redL[i]);
+      for (int i = 1; i < NW; ++i) wm = fmaxf(wm, redL[i]);
+    }
     // largest at [2^8, 2^9): every value above 2^-11 of it keeps a normal lo
     int ew = wm > 0.f && wm < INFINITY ? 9 - __builtin_amdgcn_frexp_expf(wm) : 0;
     ew = ew < -100 ? -100 : (ew > 100 ? 100 : ew);

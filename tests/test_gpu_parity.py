@@ -138,6 +138,28 @@ def test_batch_independence_bitwise():
     assert torch.equal(full[2:3], one)
 
 
+def test_batch_independence_bitwise_ragged_windows():
+    """The same at a geometry whose STW window count per sample is not a multiple of the fused
+    kernel's 8 waves per workgroup (C = 64 at latent 24, 5 frames: 3 x 6 x 6 = 108 windows), so
+    workgroups span two samples: the per-wave operand exponent (stw_x3.hip e_w) keeps every
+    sample's roundings its own (round-3 ADVICE)."""
+    cfg = pkg.spec.UnetConfig(dim=64, tc=2, tp=3, latent=24, fea_size=12)
+    x, t, cond, fea = unet_inputs(cfg, B=3, seed=9)
+    t = torch.tensor([5, 500, 950])
+    # sample 1 at a much smaller activation scale than its neighbours: a shared exponent would
+    # move its lo roundings
+    x[1] *= 1e-3
+    h = pkg._lib.Handle(cfg, 1000, 3, 0)
+    sd = make_sd(cfg)
+    sd.update(pkg.schedule_buffers(1000))
+    h.load_state(sd)
+    h.finalize()
+    full = gpu_eps(h, x, t, cond, fea)
+    for i in range(3):
+        one = gpu_eps(h, x[i:i + 1].contiguous(), t[i:i + 1], cond[i:i + 1].contiguous(), fea[i:i + 1].contiguous())
+        assert torch.equal(full[i:i + 1], one), i
+
+
 def test_ddpm_steps_vs_reference_golden():
     cfg = CONFIGS['small']
     x, _, cond, fea = unet_inputs(cfg)
