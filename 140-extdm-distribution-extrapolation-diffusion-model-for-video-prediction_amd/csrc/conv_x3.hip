@@ -764,7 +764,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
       const bool valid = q0 < a.P && row0q < a.H;
       const int q = valid ? q0 : 0, row = valid ? row0q : 0;
       const int b = q / a.T, t = q - b * a.T;
-      const int pix = PH ? (2 * row + (mtile >> 1)) * (2 * a.W) + 2 * c + (mtile & 1) : row * a.W + c;
+      // PH: the 64-row block's output phase (BM = 64: the m-tile; BM = 128: two phases of one
+      // output row parity, one per wave row)
+      const int ph = (mtile * BM + (wm * TM + i) * 32) / 64;
+      const int pix = PH ? (2 * row + (ph >> 1)) * (2 * a.W) + 2 * c + (ph & 1) : row * a.W + c;
       float v[16];
 #pragma unroll
       for (int r16 = 0; r16 < 16; ++r16) v[r16] = acc[i][j][r16] * scl[r16] + bia[r16];
@@ -774,7 +777,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
 #pragma unroll
         for (int r16 = 0; r16 < 16; ++r16)
           rv[r16] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-              rs_res, (rbase + (PH ? mrow[r16] - mtile * BM : mrow[r16]) * (int)a.e.res_sc) * 4, 0, 0));
+              rs_res, (rbase + (PH ? mrow[r16] - ph * 64 : mrow[r16]) * (int)a.e.res_sc) * 4, 0, 0));
         if (res_gn) {  // the arithmetic of gn_apply_plane_kernel (norm.hip), no FiLM
 #pragma unroll
           for (int r16 = 0; r16 < 16; ++r16) {
@@ -808,7 +811,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
       for (int r16 = 0; r16 < 16; ++r16) {
         const int m = mtile * BM + (wm * TM + i) * 32 + (r16 & 3) + 8 * (r16 >> 2) + 4 * h;
         const bool ok = valid && m < a.Cout;
-        const int off = ok ? (obase + (PH ? m - mtile * BM : m) * (int)a.oc) * 4 : a.out_bytes;
+        const int off = ok ? (obase + (PH ? m - ph * 64 : m) * (int)a.oc) * 4 : a.out_bytes;
 #if EXTDM_X3_EXP & 4
         if (v[r16] == 12345.678f)
 #endif
@@ -999,8 +1002,13 @@ X3Tile x3_tile(int ks, int cout) {
     t.bm = 64; t.bn = bn7 == 256 ? 256 : 512; t.ng = 1;
   }
   else if (ks == 5) {
-    // the phase-composed fea conv (conv_x3_phase_forward): one 64-row m-tile per output phase
-    t.bm = 64; t.bn = 512; t.ng = 1;
+    // the phase-composed fea conv (conv_x3_phase_forward): 128-row m-tiles holding both column
+    // phases of one output row parity over 256 px, so each output line is written by one
+    // workgroup and F is staged twice instead of four times (2172 -> 2026 us at B = 64, whole
+    // step -0.45 %); EXTDM_FEA_BM=64: one 64-row m-tile per phase over 512 px
+    static const int bm5 = [] { const char* v = getenv("EXTDM_FEA_BM"); return v ? atoi(v) : 128; }();
+    if (bm5 == 128) { t.bm = 128; t.bn = 256; } else { t.bm = 64; t.bn = 512; }
+    t.ng = 1;
   }
   else if (ks == 3) {
     // EXTDM_X3_BN3: pixel tile of the Cout <= 64 3x3 convs (256 or 512)
@@ -1179,7 +1187,9 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
 // EXTDM_FEA_XBUF=1: one X buffer (A/B; default two).
 bool conv_x3_phase_forward(hipStream_t s, const View& out, const View& in, const PackedW& w, const ConvEpi& epi,
                            float* edge) {
-  if (!w.wx || w.mode != MODE_CONV || w.KH != 5 || w.xbm != 64 || w.xbn != 512 || w.M != 4 * out.C) return false;
+  if (!w.wx || w.mode != MODE_CONV || w.KH != 5 || !((w.xbm == 64 && w.xbn == 512) || (w.xbm == 128 && w.xbn == 256)) ||
+      w.M != 4 * out.C || out.C != 64)
+    return false;
   if (out.H != 2 * in.H || out.W != 2 * in.W || out.B != in.B || out.T != in.T || in.C * 25 != w.K) return false;
   View og = out;  // the kernel's tile geometry: the input planes, 4C rows
   og.H = in.H; og.W = in.W; og.C = w.M;
@@ -1191,7 +1201,7 @@ bool conv_x3_phase_forward(hipStream_t s, const View& out, const View& in, const
   // per CU); default 64 x 512 on 8 waves
   static const int bn = [] { const char* v = getenv("EXTDM_FEA_TILE"); return v ? atoi(v) : 512; }();
   PackedW wt = w;
-  wt.xbn = bn == 256 ? 256 : 512;
+  if (w.xbm == 64) wt.xbn = bn == 256 ? 256 : 512;
   if (!x3_setup(og, in, nullptr, wt, e, a, ntiles, nullptr)) return false;
   auto extent = [&](long sb, long sc, long st) {
     return ((long)(out.B - 1) * sb + (long)(out.C - 1) * sc + (long)(out.T - 1) * st + (long)out.H * out.W) * 4;
@@ -1204,7 +1214,8 @@ bool conv_x3_phase_forward(hipStream_t s, const View& out, const View& in, const
   if (edge && (in.H != in.W || in.C % 16 != 0 || w.xng != 1)) return false;
   a.edge = edge;
   static const int xbuf = [] { const char* v = getenv("EXTDM_FEA_XBUF"); return v ? atoi(v) : 2; }();
-  if (wt.xbn == 512 && x3_ws_raw_ok(a, kWsPhase)) launch_sp<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true, true>(s, a, ntiles);
+  if (wt.xbm == 128) launch_sp<5, 1, 128, 256, 1, 4, 8, 2, true, 1, false, false, 0, true>(s, a, ntiles);
+  else if (wt.xbn == 512 && x3_ws_raw_ok(a, kWsPhase)) launch_sp<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true, true>(s, a, ntiles);
   else if (wt.xbn == 256) launch_sp<5, 1, 64, 256, 1, 4, 4, 1, true, 2, false, false, 0, true>(s, a, ntiles);
   else if (xbuf == 1) launch_sp<5, 1, 64, 512, 1, 8, 8, 1, true, 2, false, false, 0, true>(s, a, ntiles);
   else launch_sp<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true>(s, a, ntiles);

@@ -247,8 +247,8 @@ class NativeWorkload:
     # `kernel`: the launched template; the PMC traffic of profiles/pmc_layer<id>.json counts
     # only when it names this template and was measured on this exact library build
     # (lib_sha16).
-    LAYERS = [(0, 'mfma', 'conv_x3_kernel<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true, false>',
-               'init_conv cond_fea branch, phase-composed: 4 phases x 64 rows, 1x5x5 over the 16x16 map, 256 ch'),
+    LAYERS = [(0, 'mfma', 'conv_x3_kernel<5, 1, 128, 256, 1, 4, 8, 2, true, 1, false, false, 0, true, false>',
+               'init_conv cond_fea branch, phase-composed: 2 row parities x 2 column phases x 64 rows, 1x5x5 over the 16x16 map, 256 ch'),
               (11, 'mfma', 'fea_side_x3_kernel',
                'init_conv cond_fea branch edge corrections (2 line launches K = 5 x 256, 512 rows + corners)'),
               (1, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0, false, false>',
