@@ -124,6 +124,7 @@ template <> struct XMaxX3<7, 256> { static constexpr int v = 560; };
 template <> struct XMaxX3<3, 256> { static constexpr int v = 576; };
 template <> struct XMaxX3<3, 128> { static constexpr int v = 288; };
 template <> struct XMaxX3<1, 128> { static constexpr int v = 128; };
+template <> struct XMaxX3<1, 256> { static constexpr int v = 256; };
 template <> struct XMaxX3<7, 512> { static constexpr int v = 836; };
 template <> struct XMaxX3<3, 512> { static constexpr int v = 800; };
 template <> struct XMaxX3<5, 512> { static constexpr int v = 800; };
@@ -1021,6 +1022,7 @@ X3Tile x3_tile(int ks, int cout) {
     // staged once instead of once per 128 rows. EXTDM_X3_BM1=128 restores 128-row tiles.
     static const int bm1 = [] { const char* v = getenv("EXTDM_X3_BM1"); return v ? atoi(v) : 256; }();
     t.bm = cout <= 64 ? 64 : ((bm1 == 256 && cout % 256 == 0) ? 256 : 128);
+    // (the 256-row convs may run on 256 x 256 tiles instead: x3_bn256, chosen per launch)
     t.bn = 128; t.ng = 2;
   }
   return t;
@@ -1046,7 +1048,7 @@ bool x3_setup(const View& out, const View& in0, const View* in1, const PackedW& 
   a.RS = W + ks - 1;
   a.XPOS = a.NP * (a.TH + ks - 1) * a.RS;
   const int xmax = tl.bn == 512 ? (ks == 7 ? 836 : 800)
-                                 : (ks == 7 ? 560 : (ks == 5 ? 400 : (ks == 3 ? (tl.bn == 256 ? 576 : 288) : 128)));
+                                 : (ks == 7 ? 560 : (ks == 5 ? 400 : (ks == 3 ? (tl.bn == 256 ? 576 : 288) : (tl.bn == 256 ? 256 : 128))));
   if (a.XPOS > xmax) return false;
   a.in0 = in0.p; a.i0b = in0.sb; a.i0c = in0.sc; a.i0t = in0.st; a.C0 = in0.C;
   if (in1) { a.in1 = in1->p; a.i1b = in1->sb; a.i1c = in1->sc; a.i1t = in1->st; a.Cin = in0.C + in1->C; }
@@ -1106,8 +1108,29 @@ bool x3_mfast(const X3Args& a, const X3Tile& tl, unsigned ntiles) {
   return !off && mt > 1 && ntiles % 8 == 0 && mt * tl.bm * (long)a.Cin * 4 <= cap;
 }
 
-bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
+// 1x1 256-row convs on 256 x 256 tiles (twice the MFMAs per staged weight fragment) when that
+// tiling still fills >= 3/4 of the CUs in one round at the reference batch 64 -- a function of
+// the per-sample geometry only, like split_slices, so a clip's tiling never depends on its
+// shard (both tilings sum K in the same order: bitwise equal). The level-2 Tmodulator 460 ->
+// 353 us at B = 64; the level-3 / mid ones (56 workgroups at 256 px) keep 256 x 128 + split-K.
+// EXTDM_X3_BN1=128 keeps 256 x 128 everywhere (A/B).
+bool x3_bn256(const View& out, const PackedW& w, const ConvEpi& epi) {
+  static const int bn1 = [] { const char* v = getenv("EXTDM_X3_BN1"); return v ? atoi(v) : 256; }();
+  if (bn1 != 256 || w.KH != 1 || w.xbm != 256 || w.xbn != 128 || epi.res_aff) return false;
+  const int H = out.H, W = out.W;
+  if (W > 256 || 256 % W != 0) return false;
+  const int TH = std::min(H, 256 / W);
+  if (256 % (TH * W) != 0) return false;
+  const long NP = 256 / (TH * W), nrow = (H + TH - 1) / TH;
+  const long nwg64 = (64L * out.T + NP - 1) / NP * nrow * ((out.C + 255) / 256);
+  return nwg64 >= 192;
+}
+
+bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w0,
                      const ConvEpi& epi, int* stats_slots) {
+  PackedW wt = w0;
+  if (x3_bn256(out, w0, epi)) wt.xbn = 256;
+  const PackedW& w = wt;
   X3Args a;
   unsigned ntiles = 0;
   if (!x3_setup(out, in0, in1, w, epi, a, ntiles, stats_slots)) return false;
@@ -1160,6 +1183,7 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
     }
   }
   else if (ks == 1 && tl.bm == 64) launch<1, 1, 64, 128, 2, 4, 4, 2>(s, a, ntiles);
+  else if (ks == 1 && tl.bm == 256 && tl.bn == 256) launch<1, 1, 256, 256, 2, 2, 8, 2>(s, a, ntiles);
   else if (ks == 1 && tl.bm == 256) {
     if (x3_split256() && split_k(a, ntiles, epi, 256, 256, 256)) {
       launch_sp<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 1>(s, a, ntiles);

@@ -265,7 +265,7 @@ class NativeWorkload:
               (10, 'mfma', 'noise_pool_x3_kernel', 'init_noise_conv 3->256 1x7x7 + MaxPool(1,2,2), K = 3x49'),
               (12, 'hbm', 'pw_x3_kernel',
                'TrajWarp linear_q 256->256 1x1 + ReLU, weights register-resident (pw_x3)'),
-              (13, 'mfma', 'conv_x3_kernel<1, 1, 256, 128, 2, 2, 8, 2, true, 1, false, false, 0, false, false>',
+              (13, 'mfma', 'conv_x3_kernel<1, 1, 256, 256, 2, 2, 8, 2, true, 1, false, false, 0, false, false>',
                'level-2 MotionAdaptor Tmodulator, 1x1 over (T C) = 3584 -> 3584 channels of 8x8 px')]
     # Layers whose HBM reads are whole-line coalesced streams (every wave instruction reads >= 256
     # contiguous bytes: buffer loads of 64 consecutive pixels, 1-KB LDS-DMA pieces): their PMC
