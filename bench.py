@@ -247,6 +247,7 @@ class NativeWorkload:
     # `kernel`: the launched template; the PMC traffic of profiles/pmc_layer<id>.json counts
     # only when it names this template and was measured on this exact library build
     # (lib_sha16).
+    FP32_KERNELS = ('attn_fused_kernel', 'attn_core_kernel')
     LAYERS = [(0, 'mfma', 'conv_x3_kernel<5, 1, 128, 256, 1, 4, 8, 2, true, 1, false, false, 0, true, false>',
                'init_conv cond_fea branch, phase-composed: 2 row parities x 2 column phases x 64 rows, 1x5x5 over the 16x16 map, 256 ch'),
               (11, 'mfma', 'fea_side_x3_kernel',
@@ -318,6 +319,10 @@ class NativeWorkload:
         for layer, bound, kname, what in layers:
             if layer == 5 and self.precision == 'fp32':
                 continue
+            # the fp32 attention kernels (no f16x3 route at these head sizes / window shapes)
+            # compute in fp32 whatever the handle's precision: priced against the fp32 peak
+            fp32_kernel = kname.startswith(self.FP32_KERNELS)
+            kpeak = FP32_MFMA_PEAK_TFLOPS if fp32_kernel else peak
             try:
                 ms_layer, flops = self.h.bench_layer(B, layer, 20)
             except RuntimeError:  # the layer does not exist in this denoiser variant / precision
@@ -325,15 +330,15 @@ class NativeWorkload:
             traffic, src = self._traffic(layer, kname)
             if bound == 'mfma':
                 achieved = flops / (ms_layer * 1e-3) / 1e12
-                e = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': round(peak, 1), 'unit': 'TFLOP/s',
-                     'frac': round(achieved / peak, 4), 'flop_per_launch': flops}
+                e = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': round(kpeak, 1), 'unit': 'TFLOP/s',
+                     'frac': round(achieved / kpeak, 4), 'flop_per_launch': flops}
             else:
                 ch, hw, nt = self.HBM_BYTES[layer](u, T)
                 nbytes = 4 * B * nt * hw * ch
                 achieved = nbytes / (ms_layer * 1e-3) / 1e9
                 e = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'bytes_per_launch': nbytes}
-            e.update({'kernel': f'{kname} ({what}, {self.precision})', 'traffic': traffic, 'traffic_src': src,
+            e.update({'kernel': f"{kname} ({what}, {'fp32' if fp32_kernel else self.precision})", 'traffic': traffic, 'traffic_src': src,
                       'launch_ms': round(ms_layer, 4)})
             out.append(e)
         if not out:
