@@ -16,7 +16,7 @@ REPO = os.path.dirname(HERE)
 INCLUDE = os.path.join(REPO, 'include')
 LIB = os.path.join(HERE, 'libextdm_hip.so')
 SOURCES = ['conv.hip', 'conv_halo.hip', 'conv_x3.hip', 'pw_x3.hip', 'conv_gemm_x3.hip', 'norm.hip', 'attn.hip', 'attn_core.hip', 'stw_fused.hip',
-           'stw_x3.hip', 'cross_x3.hip', 'xpath_x3.hip', 'fea_x3.hip', 'metrics.hip', 'sampler.hip', 'decoder.hip', 'lfae.hip', 'runtime.cpp']
+           'stw_x3.hip', 'stw64_x3.hip', 'cross_x3.hip', 'xpath_x3.hip', 'fea_x3.hip', 'metrics.hip', 'sampler.hip', 'decoder.hip', 'lfae.hip', 'runtime.cpp']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-I', INCLUDE, '-I', CSRC]
 # Per-file flags. The fused f16x3 attention kernels (many independent fp32 lanes of
@@ -28,7 +28,7 @@ FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=o
 # kernel's key-tile loop: 112 copies in 441 instructions); the VGPR form of the MFMAs keeps
 # them in VGPRs (the convs' accumulators only meet VALU in the epilogue and keep AGPRs).
 VGPR_MFMA = ['-mllvm', '-amdgpu-mfma-vgpr-form=1']
-PER_FILE = {'stw_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA, 'cross_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA,
+PER_FILE = {'stw_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA, 'stw64_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA, 'cross_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA,
             'attn_core.hip': VGPR_MFMA,
             # the scaled-lo gather split as v_mul + v_fma_mixlo per value (SLP packed it into
             # v_pk_mul / v_pk_fma_f32 with the hi converted back: ~9 VALU per pair)
@@ -39,7 +39,7 @@ OPT = {}
 def _needs(obj, src):
     if not os.path.exists(obj):
         return True
-    deps = [src, os.path.join(os.path.dirname(src), 'kernels.h'), os.path.join(INCLUDE, 'extdm.h'), os.path.abspath(__file__)]
+    deps = [src, os.path.join(os.path.dirname(src), 'kernels.h'), os.path.join(os.path.dirname(src), 'attn_x3_ops.h'), os.path.join(INCLUDE, 'extdm.h'), os.path.abspath(__file__)]
     return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
 
 

@@ -303,7 +303,8 @@ bool stw_fused(hipStream_t s, const View& x, const AttnGeom& g, int heads, int d
 bool temporal_fused(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, int dim_head,
                     const float* gamma, const float* ln_w, const float* ln_b, const float* wqkv, const float* wout,
                     const float* bias_dense, int bstride, const float* rcos, const float* rsin, float q_scale);
-// f16x3 fused attention (stw_x3.hip): one wave per group of <= 32 tokens, C in {64, 128}.
+// f16x3 fused attention (stw_x3.hip): one wave per group of <= 32 tokens, C in {64, 128};
+// bf16 = the QK^T / PV contractions on bf16 MFMA (BF16_ATTN, dim_head 32).
 // Weights packed per unit of 32 qkv rows (attn_x3_unit_halves(C) halves each, see the
 // kernel header); wsc = {2^-sq, 2^-sk, 2^-sv, 2^-sproj} undoes the power-of-two pre-scaling.
 bool attn_x3_supported(int C, int ntok, int dim_head, int heads);
@@ -311,10 +312,17 @@ int attn_x3_unit_halves(int C);
 // mbias: [npat][8][32][32] bias + masks per window class (stw_x3.hip kernel header).
 bool stw_x3(hipStream_t s, const View& x, const AttnGeom& g, int heads, int dim_head, const float* gamma,
             const void* wpk, const float* wsc, const float* bp, const float* mbias, int npat,
-            const float* rcos, const float* rsin, float q_scale);
+            const float* rcos, const float* rsin, float q_scale, bool bf16);
+// f16x3 fused STW attention over windows of <= 64 tokens (stw64_x3.hip: ada / ada_u22 4x4x4
+// windows), two waves per window; the stw_x3 weight packing; mbias [npat][8][64][64] (bias +
+// masks per window class, times 2^(e_q + e_k)); bf16 = the attention contractions on bf16 MFMA.
+bool stw64_x3_supported(int C, int ntok, int dim_head, int heads);
+bool stw64_x3(hipStream_t s, const View& x, const AttnGeom& g, int heads, int dim_head, const float* gamma,
+              const void* wpk, const float* wsc, const float* bp, const float* mbias, int npat, const float* rcos,
+              const float* rsin, float q_scale, bool bf16);
 bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, int dim_head,
                  const float* gamma, const float* ln_w, const float* ln_b, const void* wpk, const float* wsc,
-                 const float* mbias, const float* rcos, const float* rsin, float q_scale);
+                 const float* mbias, const float* rcos, const float* rsin, float q_scale, bool bf16);
 // TrajWarp cross-attention (u12:719-773): q [B][256][NQ], k,v [B][256][NK].
 // f16x3 implicit-GEMM conv (conv_gemm_x3.hip): every mode / kernel size of conv_forward's
 // fp32 GEMM; false if the weight has no f16x3 GEMM packing

@@ -818,6 +818,49 @@ struct ExtdmHandle {
     mask_bias[key] = {d, npat};
     return d;
   }
+  // The same table for windows of up to 64 tokens (stw64_x3.hip): [npat][heads][64][64]
+  const float* stw_mask_bias64(const std::string& p, const AttnGeom& g, int& npat, float s2) {
+    const std::string key = p + "|64|" + std::to_string(std::ilogb(s2)) + "|" + std::to_string(g.ws0) + "," +
+                            std::to_string(g.ws1) + "," + std::to_string(g.ws2) + "|" + std::to_string(g.ss0) + "," +
+                            std::to_string(g.ss1) + "," + std::to_string(g.ss2) + "|" + std::to_string(g.Dp) + "," +
+                            std::to_string(g.Hp) + "," + std::to_string(g.Wp);
+    auto it = mask_bias.find(key);
+    if (it != mask_bias.end()) { npat = it->second.second; return it->second.first; }
+    const auto& bh = bias_host.at(p);
+    const int nh = cfg.heads, st = bh.second, N = g.ws0 * g.ws1 * g.ws2;
+    REQUIRE(N <= 64 && nh == 8 && N <= st, "bias + mask table: window of more than 64 tokens");
+    const bool shifted = (g.ss0 | g.ss1 | g.ss2) != 0;
+    npat = shifted ? 8 : 1;
+    const int ws[3] = {g.ws0, g.ws1, g.ws2}, ss[3] = {g.ss0, g.ss1, g.ss2}, P[3] = {g.Dp, g.Hp, g.Wp};
+    std::vector<float> t((size_t)npat * nh * 4096, 0.f);
+    for (int pat = 0; pat < npat; ++pat) {
+      int lab[64] = {0};
+      for (int tk = 0; tk < N; ++tk) {
+        const int tc[3] = {tk / (ws[1] * ws[2]), (tk / ws[2]) % ws[1], tk % ws[2]};
+        int l = 0;
+        for (int d = 0; d < 3; ++d) {
+          const int wi = ((pat >> d) & 1) ? P[d] / ws[d] - 1 : 0;
+          l = l * 3 + region_label(wi * ws[d] + tc[d], P[d], ws[d], ss[d]);
+        }
+        lab[tk] = l;
+      }
+      for (int hd = 0; hd < nh; ++hd)
+        for (int i = 0; i < 64; ++i)
+          for (int j = 0; j < 64; ++j) {
+            float v = 0.f;
+            if (j >= N) v = -INFINITY;
+            else if (i < N) {
+              v = bh.first[((size_t)hd * st + i) * st + j];
+              if (shifted && lab[i] != lab[j]) v += -100.f;
+            }
+            t[(((size_t)pat * nh + hd) * 64 + i) * 64 + j] = v * s2;
+          }
+    }
+    float* d = dmalloc(t.size() * 4);
+    HIPCHK(hipMemcpy(d, t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    mask_bias[key] = {d, npat};
+    return d;
+  }
   // temporal attention (one table): T5 bias of (query frame, key frame), -inf for another
   // pixel's frames and for key frames >= D (32-token groups of 32 / per pixels)
   const float* temporal_mask_bias(const AttnGeom& g, float s2) {
@@ -987,18 +1030,26 @@ struct ExtdmHandle {
     // read per call: EXTDM_NO_X3_ATTN / _STW / _TEMPORAL route a layer back to the fp32 kernels
     const bool off = flag("EXTDM_NO_X3_ATTN"), off_stw = flag("EXTDM_NO_X3_STW"), off_tmp = flag("EXTDM_NO_X3_TEMPORAL");
     if (off || (mode == 0 && off_stw) || (mode == 1 && off_tmp)) return false;
-    return cfg.precision == EXTDM_PRECISION_F16X3 && attn_x3_supported(C, ntok, cfg.dim_head, cfg.heads);
+    // BF16_ATTN: the same fused kernels with the bf16 attention core (dim_head 32)
+    return (cfg.precision == EXTDM_PRECISION_F16X3 || (bf16_attn() && cfg.dim_head == 32)) &&
+           attn_x3_supported(C, ntok, cfg.dim_head, cfg.heads);
+  }
+  // the fused 64-token-window route (stw64_x3.hip) in F16X3 and BF16_ATTN; EXTDM_NO_STW64=1 sends
+  // those windows back to the core route / fp32 fused kernels (A/B)
+  bool stw64_ok(int C, int ntok) const {
+    static const bool off = [] { const char* v = getenv("EXTDM_NO_STW64"); return v && v[0] && v[0] != '0'; }();
+    return !off && x3_convs() && stw64_x3_supported(C, ntok, cfg.dim_head, cfg.heads);
   }
   bool fused_ok(int C, int ntok) const {
     static const bool off = [] { const char* v = getenv("EXTDM_NO_FUSED_STW"); return v && v[0] && v[0] != '0'; }();
     return !off && fused_attn_supported(C, ntok, cfg.dim_head, cfg.heads);
   }
-  // the unfused core path (LN -> qkv 1x1 conv -> attn_core.hip -> proj 1x1 conv + residual):
-  // always in BF16_ATTN; in F16X3 for the shapes the fused f16x3 kernels do not cover
-  // (C = 256 windows, 64-token windows) unless EXTDM_NO_X3_CORE sends them to the fp32 fused kernels
+  // the unfused core path (LN -> qkv 1x1 conv -> attn_core.hip -> proj 1x1 conv + residual): for
+  // the shapes the fused f16x3 kernels do not cover (C = 256), in BF16_ATTN always, in F16X3 unless
+  // EXTDM_NO_X3_CORE sends them to the fp32 fused kernels
   bool core_attn(int ntok, int max_tok, bool fused_x3) const {
     if (cfg.dim_head != 32 || ntok > max_tok) return false;
-    if (bf16_attn()) return true;
+    if (bf16_attn()) return !fused_x3;
     static const bool off = [] { const char* v = getenv("EXTDM_NO_X3_CORE"); return v && v[0] && v[0] != '0'; }();
     return cfg.precision == EXTDM_PRECISION_F16X3 && !fused_x3 && !off;
   }
@@ -1015,6 +1066,19 @@ struct ExtdmHandle {
     // collapsed window reads their leading N x N block (index[:N, :N], u12:476)
     const int bstride = cfg.window[0] * cfg.window[1] * cfg.window[2] <= 32 ? 32 : 64;
     const bool fused_x3 = bstride == 32 && x3_attn_ok(x.C, N, 0);
+    if (bstride == 64 && stw64_ok(x.C, N)) {
+      // windows of up to 64 tokens (ada / ada_u22 4x4x4), one fused launch: LN, f16x3 qkv,
+      // RoPE, QK^T + bias / mask, softmax, PV (f16x3, or bf16 in BF16_ATTN), f16x3 proj + residual
+      const std::string a = p + ".fn.fn.attn";
+      const AttnX3W& w = packed_attn_x3(a + ".qkv.weight", a + ".proj.weight", p + ".fn.norm.gamma", "");
+      int npat = 1;
+      const float* mb = stw_mask_bias64(p, g, npat, w.s2);
+      if (plan) return;
+      REQUIRE(stw64_x3(s, x, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), w.w, w.sc, D(a + ".proj.bias"), mb,
+                       npat, rope_cos, rope_sin, q_scale(), bf16_attn()),
+              "f16x3 64-token STW launch rejected");
+      return;
+    }
     if (core_attn(N, 64, fused_x3)) {
       // LN + f16x3 qkv conv, the window core (bf16 or f16x3 MFMA), f16x3 proj + residual
       Scope sc(arena);
@@ -1038,7 +1102,7 @@ struct ExtdmHandle {
       const float* mb = stw_mask_bias(p, g, npat, w.s2);
       if (plan) return;
       REQUIRE(stw_x3(s, x, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), w.w, w.sc, D(a + ".proj.bias"),
-                     mb, npat, rope_cos, rope_sin, q_scale()),
+                     mb, npat, rope_cos, rope_sin, q_scale(), bf16_attn()),
               "f16x3 STW launch rejected");
       return;
     }
@@ -1097,7 +1161,7 @@ struct ExtdmHandle {
       if (plan) return;
       REQUIRE(temporal_x3(s, x, out, g, cfg.heads, cfg.dim_head, D(p + ".fn.norm.gamma"), D(a + ".norm.weight"),
                           D(a + ".norm.bias"), w.w, w.sc, mb,
-                          rope_cos, rope_sin, q_scale()),
+                          rope_cos, rope_sin, q_scale(), bf16_attn()),
               "f16x3 temporal attention launch rejected");
       return;
     }

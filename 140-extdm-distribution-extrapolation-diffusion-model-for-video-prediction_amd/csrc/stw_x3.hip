@@ -27,17 +27,14 @@
 #include <mutex>
 #include <vector>
 
-#include "kernels.h"
+#include "attn_x3_ops.h"
 
 namespace extdm {
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+using namespace attn_ops;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
-__device__ __forceinline__ int dof(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ __forceinline__ int region_label(int c, int P, int w, int s) {
   if (s == 0) return 2;
@@ -84,53 +81,6 @@ __device__ __forceinline__ Tok token_of(int tk, const AttnGeom& g, long st, int 
   return o;
 }
 
-// hi = fp16(v), lo = fp16(v - hi) of an opaque v (split_src, kernels.h): the
-// probabilities and scaled q / k / v here are products, whose two fp16 roundings hipcc
-// would otherwise lower differently (hi + lo off by an fp16 ulp in ~2^-13 of the values;
-// it made the reciprocal-multiply softmax fail at 2.7e-4).
-// CHECK: OR |v| >= 65504 (fp16 overflow of hi) into bad. Only the normalised input is
-// checked value by value; the values split inside the unit loop (q, k, v, P, O) are
-// covered by one finite check of the token's projection accumulators in the epilogue:
-// an overflowing hi is +-inf and its lo the opposite infinity, so every MFMA sum the pair
-// enters holds inf - inf = NaN, and a NaN reaches the token's output through the scores
-// (max / exp2 / sum of its own query column) and PV. Compiler-visible split2m (3 VALU per
-// pair) rather than the split2 asm (kernels.h): these splits read MFMA results and feed
-// MFMAs, and only compiler-visible VALU gets its MFMA hazard waits.
-template <bool CHECK = true>
-__device__ __forceinline__ void split8(const float* v, h8& hi, h8& lo, int& bad) {
-  float m = 0.f;
-#pragma unroll
-  for (int e = 0; e < 8; e += 2) {
-    const float w0 = split_src(v[e]), w1 = split_src(v[e + 1]);
-    if (CHECK) m = fmaxf(fmaxf(m, fabsf(w0)), fabsf(w1));
-    f16x2_t ph, pl;
-    split2m(w0, w1, ph, pl);
-    hi[e] = ph.x; hi[e + 1] = ph.y;
-    lo[e] = pl.x; lo[e + 1] = pl.y;
-  }
-  if (CHECK) bad |= m >= 65504.f;
-}
-
-__device__ __forceinline__ f32x16 mma3(const h8& ah, const h8& al, const h8& bh, const h8& bl, f32x16 c) {
-  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, c, 0, 0, 0);
-  return c;
-}
-
-// Reductions across the two half-waves (lane ^ 32) without LDS: v_permlane32_swap of v
-// with itself leaves the partner's value in r[1] of the lower lanes and in r[0] of the
-// upper lanes (own value in the other), so r[0] op r[1] is the pair's result in both
-// halves (commutative: bitwise equal).
-__device__ __forceinline__ float xh_sum(float v) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float xh_max(float v) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-
 // Packed unit slice (halves): [q: C/16 frags][k: C/16][v: C/16][proj: C/32 tiles x 2 k-steps],
 // each frag = [hl][64 lanes][8].
 template <int C>
@@ -149,7 +99,8 @@ struct UnitLayout {
 // score registers hold keys j = dof(r, h) = 8q + 4h + e (r = 4q + e): four 16-B rows of
 // its query's table row, added to the QK^T accumulator in one v_add per score (masks need
 // no further VALU). The table carries the scores' factor 2^(e_q + e_k) (wsc note).
-template <int C, int MODE, int DH, int NW, bool TILE>
+template <int C, int MODE, int DH, int NW, bool TILE, bool BF>
+// BF: the attention contractions (QK^T, PV) on bf16 MFMA (EXTDM_PRECISION_BF16_ATTN); qkv / proj stay f16x3.
 // x and out alias for the in-place STW layers (MODE 0): no __restrict__ on them.
 __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float* out,
                                                           long sb, long sc, long st, long osb, long osc, AttnGeom g,
@@ -582,15 +533,15 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       k[r] = fmaf(k0, rck[r >> 1], -(k1 * rsk[r >> 1]));
       k[r + 1] = fmaf(k1, rck[r >> 1], k0 * rsk[r >> 1]);
     }
-    h8 qf[2][2], kf[2][2], vf[2][2];  // [k-step][hi|lo]
+    Op<BF> qf[2], kf[2], vf[2];  // [k-step]
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float tq[8], tk[8], tv[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) { tq[e] = q[8 * s + e]; tk[e] = k[8 * s + e]; tv[e] = v[8 * s + e] * sv; }
-      split8<false>(tq, qf[s][0], qf[s][1], bad);
-      split8<false>(tk, kf[s][0], kf[s][1], bad);
-      split8<false>(tv, vf[s][0], vf[s][1], bad);
+      qf[s].set(tq, bad);
+      kf[s].set(tk, bad);
+      vf[s].set(tv, bad);
     }
     f32x16 o;
 #pragma unroll
@@ -605,7 +556,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       for (int r = 0; r < 16; ++r) sc_[r] = 0.f;
 #pragma unroll
       for (int s = 0; s < 2; ++s)
-        if (HPU == 1 || s == hh) sc_ = mma3(kf[s][0], kf[s][1], qf[s][0], qf[s][1], sc_);
+        if (HPU == 1 || s == hh) sc_ = mmo(kf[s], qf[s], sc_);
 #pragma unroll
       for (int r = 0; r < 16; ++r) sc_[r] += bia[hh][r];
       float mx = -INFINITY;
@@ -631,14 +582,10 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
         float tp[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) tp[e] = sc_[8 * s + e];
-        h8 ph, pl;
-        split8<false>(tp, ph, pl, bad);
-        h8 ah = vf[s][0], al = vf[s][1];
-        if (!mine) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { ah[e] = (_Float16)0.f; al[e] = (_Float16)0.f; }
-        }
-        o = mma3(ah, al, ph, pl, o);
+        Op<BF> pf, va = vf[s];
+        pf.set(tp, bad);
+        if (!mine) va.zero();
+        o = mmo(va, pf, o);
       }
     }
     return o;
@@ -892,7 +839,7 @@ bool attn_x3_tile_ok(const View& x, const View& out, const AttnGeom& g, int grou
          x.st == (long)x.H * x.W && x.sc % 4 == 0 && x.sb % 4 == 0 && ((uintptr_t)x.p & 15) == 0;
 }
 
-template <int C, int MODE, int DH, int NW>
+template <int C, int MODE, int DH, int NW, bool BF>
 void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int groups, const float* gamma,
                const float* lw, const float* lb, const void* wpk, const float* wsc, const float* bp,
                const float* mbias, int npat, const float* rcos, const float* rsin, float q_scale) {
@@ -913,10 +860,10 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::call_once(once[dev & 63], [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW, false>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW, false, BF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (C == 64 && NW == 8)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW, C == 64 && NW == 8>),
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_x3_kernel<C, MODE, DH, NW, C == 64 && NW == 8, BF>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
   const int total = x.B * groups;
@@ -927,7 +874,7 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
     (void)hipMemsetAsync(ts, 0, (size_t)total * 24 * sizeof(long long), s);
   }
   constexpr bool TILE_OK = C == 64 && NW == 8;
-  auto kern = tile ? &attn_x3_kernel<C, MODE, DH, NW, TILE_OK> : &attn_x3_kernel<C, MODE, DH, NW, false>;
+  auto kern = tile ? &attn_x3_kernel<C, MODE, DH, NW, TILE_OK, BF> : &attn_x3_kernel<C, MODE, DH, NW, false, BF>;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, s, x.p, out.p, x.sb, x.sc, x.st, out.sb, out.sc, g, gamma,
                      lw, lb, reinterpret_cast<const _Float16*>(wpk), wsc, bp, mbias, npat, rcos, rsin, q_scale, groups,
                      total, x3_range_ptr(), dbg, ts);
@@ -944,7 +891,7 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
       ++n;
       for (int k = 1; k < 20; ++k) acc[k] += (double)(t[k] - t[k - 1]);
     }
-    fprintf(stderr, "attn_x3<C=%d,MODE=%d,DH=%d,NW=%d> stamps over %ld waves (cycles): prologue %.0f", C, MODE, DH, NW, n,
+    fprintf(stderr, "attn_x3<C=%d,MODE=%d,DH=%d,NW=%d,BF> stamps over %ld waves (cycles): prologue %.0f", C, MODE, DH, NW, n,
             acc[1] / n);
     for (int u = 0; u < 8; ++u) fprintf(stderr, " | u%d wait %.0f body %.0f", u, acc[3 + 2 * u] / n, acc[4 + 2 * u] / n);
     fprintf(stderr, " | tail %.0f epilogue %.0f", acc[18] / n, acc[19] / n);
@@ -960,24 +907,35 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
   }
 }
 
-template <int C, int MODE, int DH>
+template <int C, int MODE, int DH, bool BF>
 void launch(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int groups, const float* gamma,
             const float* lw, const float* lb, const void* wpk, const float* wsc, const float* bp,
             const float* mbias, int npat, const float* rcos, const float* rsin, float q_scale) {
   static const int nw = [] { const char* v = getenv("EXTDM_X3_ATTN_NW"); return v ? atoi(v) : 0; }();
   // C = 128 needs > 256 VGPRs: one wave per SIMD
   if (C == 64 && nw != 4)
-    launch_nw<C, MODE, DH, 8>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
+    launch_nw<C, MODE, DH, 8, BF>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
   else
-    launch_nw<C, MODE, DH, 4>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
+    launch_nw<C, MODE, DH, 4, BF>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
 }
 
+// bf16: the BF16_ATTN attention core, instantiated for dim_head 32 (attn_x3_supported)
 template <int MODE, int DH>
 bool dispatch_c(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int groups, const float* gamma,
                 const float* lw, const float* lb, const void* wpk, const float* wsc, const float* bp,
-                const float* mbias, int npat, const float* rcos, const float* rsin, float q_scale) {
-  if (x.C == 64) launch<64, MODE, DH>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
-  else if (x.C == 128) launch<128, MODE, DH>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
+                const float* mbias, int npat, const float* rcos, const float* rsin, float q_scale, bool bf16) {
+  if constexpr (DH == 32) {
+    if (bf16) {
+      if (x.C == 64) launch<64, MODE, DH, true>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
+      else if (x.C == 128) launch<128, MODE, DH, true>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
+      else return false;
+      return true;
+    }
+  } else {
+    if (bf16) return false;
+  }
+  if (x.C == 64) launch<64, MODE, DH, false>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
+  else if (x.C == 128) launch<128, MODE, DH, false>(s, x, out, g, groups, gamma, lw, lb, wpk, wsc, bp, mbias, npat, rcos, rsin, q_scale);
   else return false;
   return true;
 }
@@ -1001,20 +959,20 @@ static bool extent_ok(const View& v, const AttnGeom& g) {
 
 bool stw_x3(hipStream_t s, const View& x, const AttnGeom& g, int heads, int dim_head, const float* gamma,
             const void* wpk, const float* wsc, const float* bp, const float* mbias, int npat,
-            const float* rcos, const float* rsin, float q_scale) {
+            const float* rcos, const float* rsin, float q_scale, bool bf16) {
   const int N = g.ws0 * g.ws1 * g.ws2;
   if (!attn_x3_supported(x.C, N, dim_head, heads) || !extent_ok(x, g)) return false;
   const int groups = (g.Dp / g.ws0) * (g.Hp / g.ws1) * (g.Wp / g.ws2);
   if (dim_head == 32)
     return dispatch_c<0, 32>(s, x, x, g, groups, gamma, nullptr, nullptr, wpk, wsc, bp, mbias, npat, rcos,
-                             rsin, q_scale);
+                             rsin, q_scale, bf16);
   return dispatch_c<0, 16>(s, x, x, g, groups, gamma, nullptr, nullptr, wpk, wsc, bp, mbias, npat, rcos, rsin,
-                           q_scale);
+                           q_scale, bf16);
 }
 
 bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& g, int heads, int dim_head,
                  const float* gamma, const float* ln_w, const float* ln_b, const void* wpk, const float* wsc,
-                 const float* mbias, const float* rcos, const float* rsin, float q_scale) {
+                 const float* mbias, const float* rcos, const float* rsin, float q_scale, bool bf16) {
   const int npat = 1;
   if (!attn_x3_supported(x.C, g.D, dim_head, heads) || g.D > 32 || !extent_ok(x, g) || !extent_ok(out, g)) return false;
   if (out.sc != x.sc || out.st != x.st) return false;
@@ -1022,9 +980,9 @@ bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& 
   const int groups = (g.H * g.W + ppb - 1) / ppb;
   if (dim_head == 32)
     return dispatch_c<1, 32>(s, x, out, g, groups, gamma, ln_w, ln_b, wpk, wsc, nullptr, mbias, npat, rcos,
-                             rsin, q_scale);
+                             rsin, q_scale, bf16);
   return dispatch_c<1, 16>(s, x, out, g, groups, gamma, ln_w, ln_b, wpk, wsc, nullptr, mbias, npat, rcos, rsin,
-                           q_scale);
+                           q_scale, bf16);
 }
 
 }  // namespace extdm

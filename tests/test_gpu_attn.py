@@ -103,3 +103,54 @@ def test_attention_core_heads6_vs_oracle(prefix, level, shifted):
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), out2.cpu())
     assert err <= 2e-5, err
+
+
+# 64-token windows (ada / ada_u22 4x4x4): the fused stw64_x3 route. ada_kth: dim_head 16 (two
+# heads per 32-row unit), T = 30 -> padded to 32 frames; u22_city: dim_head 32, T = 7 -> 8
+# (a padded frame inside every window of the last window row). `level`: the latent halvings
+# (C 64 / 128 from the weights; ups.2.1 is C 64 at latent / 2).
+W64 = [('ada_kth', 'downs.0.1', 0, True), ('ada_kth', 'downs.0.3', 0, False), ('ada_kth', 'downs.1.1', 1, True),
+       ('u22_city', 'downs.0.1', 0, True), ('u22_city', 'downs.1.3', 1, False), ('u22_city', 'ups.2.1', 1, True)]
+
+
+def _w64_case(name, prefix, level, shifted, precision):
+    from oracle import extdm_oracle as O
+    cfg = CONFIGS[name]
+    h, sd = handle(name, precision)
+    C = sd[prefix + '.fn.fn.attn.qkv.weight'].shape[1]  # ups.i sit one level above their channels
+    L = cfg.latent >> level
+    gen = torch.Generator().manual_seed(25 + level)
+    x = torch.randn(2, C, cfg.frames, L, L, generator=gen) * 1.5 + 0.3
+    out = torch.empty(x.shape, device=DEV)
+    h.attn_layer(prefix, x.to(DEV), out, shifted=shifted)
+    torch.cuda.synchronize()
+    win = tuple(cfg.window)
+    with torch.no_grad():
+        ref = O.stw_attention(sd, prefix, x, win, tuple(w // 2 for w in win) if shifted else (0, 0, 0),
+                              cfg.heads, cfg.dim_head)
+    out2 = torch.empty(x.shape, device=DEV)
+    h.attn_layer(prefix, x.to(DEV), out2, shifted=shifted)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), out2.cpu())  # bit-stable across launches
+    return x, out.cpu(), ref
+
+
+@pytest.mark.parametrize('name,prefix,level,shifted', W64)
+def test_window64_attention_vs_oracle(name, prefix, level, shifted):
+    """f16x3 (fp32-faithful): the same 2e-5 bar as the <= 32-token windows."""
+    x, out, ref = _w64_case(name, prefix, level, shifted, 'f16x3')
+    err = (out - ref).abs().max().item()
+    print(f'{name} {prefix} f16x3 max|err| {err:.3e}')
+    assert err <= 2e-5, err
+
+
+@pytest.mark.parametrize('name,prefix,level,shifted', W64)
+def test_window64_attention_bf16_vs_oracle(name, prefix, level, shifted):
+    """bf16 attention contractions (BF16_ATTN): q, k, v and P rounded to bf16 (2^-9 relative
+    each). Bar: max-abs <= 1e-2 x max|attention increment| (ref - x)."""
+    x, out, ref = _w64_case(name, prefix, level, shifted, 'bf16_attn')
+    err = (out - ref).abs().max().item()
+    inc = (ref - x).abs().max().item()
+    print(f'{name} {prefix} bf16_attn max|err| {err:.3e} = {err / inc:.2e} x max|increment|')
+    assert err <= 1e-2 * inc, (err, inc)
+    assert err > 1e-7  # a different arithmetic from the fp32-faithful mode
