@@ -9,7 +9,7 @@ LIB_PATH = os.environ.get('EXTDM_LIB') or os.path.join(HERE, 'libextdm_hip.so')
 
 # every symbol include/extdm.h declares
 EXPORTS = ['extdm_create', 'extdm_destroy', 'extdm_last_error', 'extdm_load_weight', 'extdm_finalize',
-           'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_bench_layer',
+           'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_bench_layer', 'extdm_bench_layer_kernel',
            'extdm_decode', 'extdm_set_lfae', 'extdm_region_params', 'extdm_region_hw', 'extdm_bg_params',
            'extdm_flow_predict', 'extdm_flow_hw', 'extdm_bottleneck', 'extdm_range_flag',
            'extdm_attn_layer', 'extdm_frame_metrics_workspace', 'extdm_frame_metrics', 'extdm_bilinear_frames']
@@ -77,6 +77,8 @@ def load():
     L.extdm_sampler_step.restype = i32
     L.extdm_bench_layer.argtypes = [vp, i32, i32, i32, ctypes.POINTER(f32), ctypes.POINTER(ctypes.c_double)]
     L.extdm_bench_layer.restype = i32
+    L.extdm_bench_layer_kernel.argtypes = [vp, i32, ctypes.c_char_p, i32]
+    L.extdm_bench_layer_kernel.restype = i32
     L.extdm_decode.argtypes = [vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]
     L.extdm_decode.restype = i32
     L.extdm_set_lfae.argtypes = [vp, ctypes.POINTER(ExtdmLfaeConfig)]
@@ -265,6 +267,12 @@ class Handle:
         ms, fl = ctypes.c_float(), ctypes.c_double()
         check(load().extdm_bench_layer(self.h, B, layer, iters, ctypes.byref(ms), ctypes.byref(fl)))
         return float(ms.value), float(fl.value)
+
+    def bench_layer_kernel(self, layer):
+        """The kernel template the last bench_layer(layer) launched ('' if not recorded)."""
+        buf = ctypes.create_string_buffer(256)
+        check(load().extdm_bench_layer_kernel(self.h, layer, buf, 256))
+        return buf.value.decode()
 
     # ---- LFAE encoder (include/extdm.h, SURVEY §8 a22) ----
     def set_lfae(self, lc):

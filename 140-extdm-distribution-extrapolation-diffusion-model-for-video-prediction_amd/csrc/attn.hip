@@ -242,6 +242,7 @@ void window_attention(hipStream_t s, const View& qkv, const View& o, const AttnG
   unsigned nblocks;
   if (g.mode == 0) nblocks = (unsigned)(qkv.B * (g.Dp / g.ws0) * (g.Hp / g.ws1) * (g.Wp / g.ws2));
   else nblocks = (unsigned)(qkv.B * g.H * g.W);
+  note_kernel("window_attn_kernel");
   hipLaunchKernelGGL(window_attn_kernel, dim3(nblocks), dim3(256), 0, s, qkv.p, qkv.sb, qkv.sc, o.p, o.sb, o.sc, g,
                      heads, bias_dense, rope_cos, rope_sin, q_scale, qkv.st);
 }

@@ -309,8 +309,11 @@ bool attention_core(hipStream_t s, const View& qkv, const View& o, const AttnGeo
   const int total = qkv.B * groups;
   int* flag = x3_range_ptr();
 #define CORE_GO(M, X, NT_)                                                                                   \
+  do {                                                                                                       \
+  note_kernel("attn_core_kernel<%d, %s, %d>", M, X ? "true" : "false", NT_);                                  \
   hipLaunchKernelGGL((attn_core_kernel<M, X, NT_>), dim3(total), dim3(256), 0, s, qkv.p, qkv.sb, qkv.sc, qkv.st,  \
-                     o.p, o.sb, o.sc, g, heads, groups, total, bias_dense, bstride, rope_cos, rope_sin, q_scale, flag)
+                     o.p, o.sb, o.sc, g, heads, groups, total, bias_dense, bstride, rope_cos, rope_sin, q_scale, flag); \
+  } while (0)
   if (g.mode == 0 && nt == 2) {
     if (bf16) CORE_GO(0, false, 2);
     else CORE_GO(0, true, 2);

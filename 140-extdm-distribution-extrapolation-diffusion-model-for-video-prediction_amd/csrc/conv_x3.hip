@@ -1208,9 +1208,10 @@ bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View
 // (runtime.cpp Pfea_phase): the 7x7 over the 2H x 2W upsampled map equals, per output phase
 // (py, px), a 5x5 over the zero-padded H x W map F plus edge corrections (fea_x3.hip). This
 // launch is the 5x5 part: Cout = 4 phases x C rows, out [B][C][T][2H][2W] (+= epi.res).
-// EXTDM_FEA_XBUF=1: one X buffer (A/B; default two).
+// EXTDM_FEA_XBUF=1: one X buffer (A/B; default two). dry: return whether the launch is covered
+// (every check above, no launch).
 bool conv_x3_phase_forward(hipStream_t s, const View& out, const View& in, const PackedW& w, const ConvEpi& epi,
-                           float* edge) {
+                           float* edge, bool dry) {
   if (!w.wx || w.mode != MODE_CONV || w.KH != 5 || !((w.xbm == 64 && w.xbn == 512) || (w.xbm == 128 && w.xbn == 256)) ||
       w.M != 4 * out.C || out.C != 64)
     return false;
@@ -1237,6 +1238,7 @@ bool conv_x3_phase_forward(hipStream_t s, const View& out, const View& in, const
   a.res_bytes = (int)rb;
   if (edge && (in.H != in.W || in.C % 16 != 0 || w.xng != 1)) return false;
   a.edge = edge;
+  if (dry) return true;  // coverage only (runtime.cpp fea_phase_on)
   static const int xbuf = [] { const char* v = getenv("EXTDM_FEA_XBUF"); return v ? atoi(v) : 2; }();
   if (wt.xbm == 128) launch_sp<5, 1, 128, 256, 1, 4, 8, 2, true, 1, false, false, 0, true>(s, a, ntiles);
   else if (wt.xbn == 512 && x3_ws_raw_ok(a, kWsPhase)) launch_sp<5, 1, 64, 512, 1, 8, 8, 2, true, 2, false, false, 0, true, true>(s, a, ntiles);

@@ -292,11 +292,12 @@ bool fea_edges_supported(int C, int Co, int L) {
 }
 
 bool fea_edges_forward(hipStream_t s, const View& out, const float* edge, int C, const void* side_w,
-                       const float* side_scale, const float* corner_w) {
+                       const float* side_scale, const float* corner_w, bool dry) {
   const int L = out.H / 2, Co = out.C;
   if (out.W != out.H || out.H % 2 != 0 || !fea_edges_supported(C, Co, L)) return false;
   const long ext = ((long)(out.B - 1) * out.sb + (long)(Co - 1) * out.sc + (long)(out.T - 1) * out.st + 4L * L * L) * 4;
   if (ext >= (1L << 31) - 4) return false;
+  if (dry) return true;
   FeaSideArgs a{};
   a.e = edge;
   a.C = C; a.L = L; a.T = out.T; a.P = out.B * out.T;

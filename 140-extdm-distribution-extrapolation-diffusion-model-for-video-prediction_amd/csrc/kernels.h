@@ -96,6 +96,11 @@ __device__ __forceinline__ void amax2(float& m, float a, float b) {
   asm("v_max3_f32 %0, |%1|, |%2|, %0" : "+v"(m) : "v"(a), "v"(b));
 }
 
+// The template of the last attention launch on this thread (extdm_bench_layer_kernel: bench.py
+// prices a layer by the arithmetic of the kernel it actually launched). printf-style.
+void note_kernel(const char* fmt, ...);
+const char* noted_kernel();
+
 struct View {
   float* p = nullptr;
   int B = 0, C = 0, T = 0, H = 0, W = 0;
@@ -204,7 +209,7 @@ bool conv_x3_forward_op(hipStream_t s, const View& out, const X3Op& in, const Pa
 // (fea_x3.hip header): the 5x5 part, out [B][Co][T][2H][2W] += (epi.res), weights [4 Co][C][5][5]
 // edge (non-null): F's four edge lines are written to edge [B*T][4][H][C] (fea_edge_floats)
 bool conv_x3_phase_forward(hipStream_t s, const View& out, const View& in, const PackedW& w, const ConvEpi& epi,
-                           float* edge = nullptr);
+                           float* edge = nullptr, bool dry = false);
 // ... and its edge corrections from those lines, added into out (after the 5x5 launch):
 // side_w / side_scale the packed f16x3 line weights [pair][side][mtile][cb][tap][m32][hl][lane][8]
 // / row scales [pair][side][mt * 128], corner_w fp32 [corner][C][Co][16 px]
@@ -225,7 +230,7 @@ struct FeaCornerArgs {
 inline size_t fea_edge_floats(int P, int C, int L) { return (size_t)P * 4 * L * C; }
 bool fea_edges_supported(int C, int Co, int L);
 bool fea_edges_forward(hipStream_t s, const View& out, const float* edge, int C, const void* side_w,
-                       const float* side_scale, const float* corner_w);
+                       const float* side_scale, const float* corner_w, bool dry = false);
 void x3_range_reset(hipStream_t s);
 // 1x1 256 -> 256 f16x3 conv with register-resident weights (pw_x3.hip) on conv_x3's packed 1x1
 // weights (xbm 256): single input view, HW % 64 == 0, epilogue bias + ReLU only (no residual,

@@ -10,6 +10,8 @@
 #include <algorithm>
 #include <functional>
 #include <cmath>
+#include <cstdarg>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -498,6 +500,29 @@ struct ExtdmHandle {
     const int fs = cfg.fea_size;
     return !off && xpath_enabled() && cfg.dim == 64 && cfg.latent == 2 * fs && (fs == 16 || fs == 32) &&
            fea_edges_supported(cfg.fea_ch, cfg.dim, fs);
+  }
+  // fea_phase_enabled() and both launches covered at max_batch (the same checks as the
+  // launchers, dry run: 31-bit output / residual extents, the tile / x3_setup limits), decided
+  // once per handle so that the planned workspace and every forward take the same route; where
+  // not covered the forward keeps the bilinear upsample and the 7x7 conv (round-4 ADVICE).
+  int fea_phase_state = -1;
+  bool fea_phase_on() {
+    if (fea_phase_state >= 0) return fea_phase_state != 0;
+    bool ok = fea_phase_enabled();
+    if (ok) {
+      const FeaPhaseW& fw = Pfea_phase();
+      const PackedW& w5 = P("init_conv.weight#fea5");
+      const int Bm = cfg.max_batch, T = frames(), L = cfg.latent, fs = cfg.fea_size;
+      float* fake = reinterpret_cast<float*>(uintptr_t(1) << 20);  // never dereferenced (dry run)
+      const View rp = cf_view(fake, Bm, cfg.dim, T, L, L).frames(tm(), cfg.tp);
+      const View f = cf_view(fake, Bm, cfg.fea_ch, cfg.tp, fs, fs);
+      ConvEpi e;
+      e.res = rp.p; e.res_sb = rp.sb; e.res_sc = rp.sc; e.res_st = rp.st;
+      ok = conv_x3_phase_forward(nullptr, rp, f, w5, e, fake, true) &&
+           fea_edges_forward(nullptr, rp, fake, cfg.fea_ch, fw.side, fw.side_scale, fw.corner, true);
+    }
+    fea_phase_state = ok ? 1 : 0;
+    return ok;
   }
   // up2 of a length-n axis, align_corners=False, as F.interpolate: weight of F[k] in row r
   // (0 outside [0, 2n): the 7x7's zero padding), and the unclamped interpolation of the
@@ -1058,6 +1083,13 @@ struct ExtdmHandle {
   int tm() const { return cfg.arch == EXTDM_ARCH_WO_REF ? cfg.tc - 1 : cfg.tc; }
   int frames() const { return tm() + cfg.tp; }
 
+  // extdm_bench_layer on the unfused core route: 0 = the whole layer, 1 = the attention core
+  // alone, 2 = the qkv 1x1 conv alone, 3 = the proj / to_out 1x1 conv alone (the other launches
+  // skipped; their buffers hold the warm-up run's values). last_core: the route taken.
+  int bench_stage = 0;
+  bool last_core = false;
+  std::unordered_map<int, std::string> bench_kernel;  // bench layer id -> launched template
+
   // Residual(PreNorm(STWAttentionLayer)) in place on x (u12:498-559, 961-963)
   void stw(const std::string& p, const View& x, bool shifted) {
     const AttnGeom g = stw_geom(x.T, x.H, x.W, shifted);
@@ -1081,18 +1113,21 @@ struct ExtdmHandle {
     }
     if (core_attn(N, 64, fused_x3)) {
       // LN + f16x3 qkv conv, the window core (bf16 or f16x3 MFMA), f16x3 proj + residual
+      // (bench_stage: extdm_bench_layer times one of the three launches alone)
+      last_core = true;
       Scope sc(arena);
       const int hid = cfg.heads * 32;
       View ln = alloc_cf(x.B, x.C, x.T, x.H, x.W);
-      if (!plan) channel_ln(s, ln, x, nullptr, D(p + ".fn.norm.gamma"));
+      if (!plan && bench_stage == 0) channel_ln(s, ln, x, nullptr, D(p + ".fn.norm.gamma"));
       View qkv = alloc_cf(x.B, 3 * hid, x.T, x.H, x.W);
-      conv(qkv, ln, nullptr, P(p + ".fn.fn.attn.qkv.weight"), 1, 0, nullptr);
+      if (bench_stage == 0 || bench_stage == 2) conv(qkv, ln, nullptr, P(p + ".fn.fn.attn.qkv.weight"), 1, 0, nullptr);
       View o = alloc_cf(x.B, hid, x.T, x.H, x.W);
-      if (!plan)
+      if (!plan && (bench_stage == 0 || bench_stage == 1))
         REQUIRE(attention_core(s, qkv, o, g, cfg.heads, cfg.dim_head, bias_dense.at(p), bstride, rope_cos, rope_sin,
                                q_scale(), bf16_attn()),
                 "STW attention core launch rejected");
-      conv(x, o, nullptr, P(p + ".fn.fn.attn.proj.weight"), 1, 0, D(p + ".fn.fn.attn.proj.bias"), &x);
+      if (bench_stage == 0 || bench_stage == 3)
+        conv(x, o, nullptr, P(p + ".fn.fn.attn.proj.weight"), 1, 0, D(p + ".fn.fn.attn.proj.bias"), &x);
       return;
     }
     if (fused_x3) {
@@ -1140,18 +1175,20 @@ struct ExtdmHandle {
     const bool fused_x3 = x3_attn_ok(x.C, T, 1) && out.sc == x.sc && out.st == x.st;
     if (core_attn(T, 32, fused_x3)) {
       // double-LN prologue, f16x3 qkv conv, the core (bf16 or f16x3 MFMA), f16x3 to_out + residual
+      last_core = true;
       Scope sc(arena);
       const int hid = cfg.heads * 32;
       View z = alloc_cf(x.B, x.C, T, x.H, x.W), rr = alloc_cf(x.B, x.C, T, x.H, x.W);
-      if (!plan) temporal_prologue(s, x, D(p + ".fn.norm.gamma"), D(a + ".norm.weight"), D(a + ".norm.bias"), z, rr);
+      if (!plan && bench_stage == 0)
+        temporal_prologue(s, x, D(p + ".fn.norm.gamma"), D(a + ".norm.weight"), D(a + ".norm.bias"), z, rr);
       View qkv = alloc_cf(x.B, 3 * hid, T, x.H, x.W);
-      conv(qkv, z, nullptr, P(a + ".attn.to_qkv.weight"), 1, 0, nullptr);
+      if (bench_stage == 0 || bench_stage == 2) conv(qkv, z, nullptr, P(a + ".attn.to_qkv.weight"), 1, 0, nullptr);
       View o = alloc_cf(x.B, hid, T, x.H, x.W);
-      if (!plan)
+      if (!plan && (bench_stage == 0 || bench_stage == 1))
         REQUIRE(attention_core(s, qkv, o, g, cfg.heads, cfg.dim_head, time_bias, 32, rope_cos, rope_sin, q_scale(),
                                bf16_attn()),
                 "temporal attention core launch rejected");
-      conv(out, o, nullptr, P(a + ".attn.to_out.weight"), 1, 0, nullptr, &rr);
+      if (bench_stage == 0 || bench_stage == 3) conv(out, o, nullptr, P(a + ".attn.to_out.weight"), 1, 0, nullptr, &rr);
       return;
     }
     if (fused_x3) {
@@ -1314,7 +1351,7 @@ struct ExtdmHandle {
     }
     if (cfg.arch == EXTDM_ARCH_ADA || cfg.arch == EXTDM_ARCH_ADA_U22)
       fup_all = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * T * L * L * 4), Bm, cfg.fea_ch, T, L, L);
-    if (cfg.arch == EXTDM_ARCH_ADA && fea_phase_enabled())
+    if (cfg.arch == EXTDM_ARCH_ADA && fea_phase_on())
       fa_all = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * T * fs * fs * 4), Bm, cfg.fea_ch, T, fs, fs);
   }
   static View with_batch(View v, int B) { v.B = B; return v; }
@@ -1418,7 +1455,7 @@ struct ExtdmHandle {
           View fp2 = alloc_cf(B, cfg.fea_ch, tp, fs, fs);
           trajwarp_q(xq, vf, fp2);
           fpre = fp2;
-          if (!fea_phase_enabled()) {
+          if (!fea_phase_on()) {
             fu = alloc_cf(B, cfg.fea_ch, tp, L, L);
             if (!plan) bilinear_frames(s, fu, fp2, fp2, 0);
           }
@@ -1430,7 +1467,7 @@ struct ExtdmHandle {
           // rp = K_class * x + cbias_class (x-branch + both biases), then rp += Wb * pad(up2(F))
           const XPathW& xw = Pxpath();
           if (!plan) REQUIRE(xpath_x3_forward(s, rp, xpad, xw.w, xw.rs, xw.cb), "composed init_conv launch rejected");
-          if (fea_phase_enabled()) fea_phase_conv(rp, fpre);  // over F itself (fea_x3.hip)
+          if (fea_phase_on()) fea_phase_conv(rp, fpre);  // over F itself (fea_x3.hip)
           else conv(rp, fu, nullptr, P("init_conv.weight#fea"), 1, 3, nullptr, &rp);
         } else {
           conv(rp, x0p, &fu, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
@@ -2083,6 +2120,19 @@ int guarded(F&& f) {
 }
 }  // namespace
 
+namespace extdm {
+static thread_local std::string g_noted_kernel;
+void note_kernel(const char* fmt, ...) {
+  char buf[256];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_noted_kernel = buf;
+}
+const char* noted_kernel() { return g_noted_kernel.c_str(); }
+}  // namespace extdm
+
 extern "C" {
 
 const char* extdm_last_error(void) { return g_last_error.c_str(); }
@@ -2355,23 +2405,44 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
       *flops_out = flop;
       return;
     }
-    if (layer >= 6 && layer <= 8) {
+    if ((layer >= 6 && layer <= 8) || (layer >= 14 && layer <= 17)) {
       const int C = h->cfg.dim;
       double flop = 0;
       std::function<void()> launch;
       View x = h->alloc_cf(B, C, T, L, L), o = h->alloc_cf(B, C, T, L, L);
       fill_normal(s, x.p, 1, (int)x.numel(), 17, 0, 0, 3);
       const int hid = h->cfg.heads * h->cfg.dim_head;
-      if (layer == 6) {
-        REQUIRE(h->has("downs.0.1.fn.fn.attn.qkv.weight"), "bench layer 6: no level-0 STW layer");
+      // 6 / 7: the level-0 STW / init_temporal attention layer — one fused launch, or on the
+      // unfused core route the attention core alone (14 / 16: its qkv 1x1 conv, 15 / 17: its
+      // proj / to_out 1x1 conv, each timed alone)
+      const bool stw_l = layer == 6 || layer == 14 || layer == 15;
+      const int stage = layer == 6 || layer == 7 ? 1 : (layer == 14 || layer == 16 ? 2 : 3);
+      if (stw_l || layer == 7 || layer == 16 || layer == 17) {
+        const char* need = stw_l ? "downs.0.1.fn.fn.attn.qkv.weight" : "init_temporal_attn.fn.fn.fn.attn.to_qkv.weight";
+        REQUIRE(h->has(need), std::string("bench layer ") + std::to_string(layer) + ": no such attention layer");
         const AttnGeom g = h->stw_geom(T, L, L, true);
-        const int N = g.ws0 * g.ws1 * g.ws2;
-        flop = (double)B * T * L * L * (2.0 * C * 3 * hid + 4.0 * N * hid + 2.0 * hid * C);
-        launch = [&] { h->stw("downs.0.1", x, true); };
-      } else if (layer == 7) {
-        REQUIRE(h->has("init_temporal_attn.fn.fn.fn.attn.to_qkv.weight"), "bench layer 7: no temporal layer");
-        flop = (double)B * T * L * L * (2.0 * C * 3 * hid + 4.0 * T * hid + 2.0 * hid * C);
-        launch = [&] { h->temporal("init_temporal_attn", x, o); };
+        const int N = stw_l ? g.ws0 * g.ws1 * g.ws2 : T;
+        h->last_core = false;
+        h->bench_stage = 0;
+        if (stw_l) h->stw("downs.0.1", x, true);  // warm (packs weights / tables) and probes the route
+        else h->temporal("init_temporal_attn", x, o);
+        const bool core = h->last_core;
+        REQUIRE(core || layer == 6 || layer == 7, "bench layer " + std::to_string(layer) + ": the layer is one fused launch");
+        const double tok = (double)B * T * L * L;
+        const double f_qkv = tok * 2.0 * C * 3 * hid, f_core = tok * 4.0 * N * hid, f_proj = tok * 2.0 * hid * C;
+        flop = !core ? f_qkv + f_core + f_proj : stage == 1 ? f_core : stage == 2 ? f_qkv : f_proj;
+        const int st_ = core ? stage : 0;
+        launch = [&, stw_l, st_] {
+          h->bench_stage = st_;
+          if (stw_l) h->stw("downs.0.1", x, true);
+          else h->temporal("init_temporal_attn", x, o);
+          h->bench_stage = 0;
+        };
+        note_kernel("");
+        launch();
+        h->bench_kernel[layer] = noted_kernel();
+      } else if (layer == 6 || layer == 7) {
+        // unreachable (handled above)
       } else {
         REQUIRE(h->cfg.arch == EXTDM_ARCH_U12 && h->kv_split_ok(), "bench layer 8: no pre-split TrajWarp cross-attention");
         const int fs = h->cfg.fea_size, Cf = h->cfg.fea_ch, nq = h->cfg.tp * fs * fs, nk = h->cfg.tc * fs * fs;
@@ -2404,7 +2475,7 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     // layers 0 / 11 with the phase-composed cond_fea branch (fea_x3.hip): 0 = the 5x5 phase conv
     // over F (fea_size, 4 x dim rows, += into r as the forward issues it), 11 = its edge
     // corrections (the two line launches and the corner launch)
-    if ((layer == 0 || layer == 11) && h->fea_phase_enabled()) {
+    if ((layer == 0 || layer == 11) && h->fea_phase_on()) {
       const int fs = h->cfg.fea_size, Cf = h->cfg.fea_ch, Co = h->cfg.dim;
       View f = h->alloc_cf(B, Cf, T, fs, fs), r = h->alloc_cf(B, Co, T, L, L);
       float* edge = h->arena.alloc(fea_edge_floats(B * T, Cf, fs));
@@ -2539,6 +2610,15 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     (void)hipEventDestroy(b);
     *ms_out = ms / iters;
     *flops_out = 2.0 * B * T * Lq * Lq * (double)co * ci * ks * ks;
+  });
+}
+
+int extdm_bench_layer_kernel(ExtdmHandle* h, int layer, char* buf, int cap) {
+  return guarded([&] {
+    REQUIRE(h && buf && cap > 0, "bench_layer_kernel: arguments");
+    auto it = h->bench_kernel.find(layer);
+    const std::string v = it == h->bench_kernel.end() ? std::string() : it->second;
+    std::snprintf(buf, (size_t)cap, "%s", v.c_str());
   });
 }
 

@@ -399,6 +399,7 @@ void launch(hipStream_t s, const View& x, const AttnGeom& g, int groups, const f
   });
   const int total = x.B * groups;
   const int grid = (total + NW / 2 - 1) / (NW / 2);
+  note_kernel("stw64_x3_kernel<%d, %d, %d, %s>", C, DH, NW, BF ? "true" : "false");
   hipLaunchKernelGGL((stw64_x3_kernel<C, DH, NW, BF>), dim3(grid), dim3(NW * 64), lds, s, x.p, x.sb, x.sc, x.st, g,
                      gamma, reinterpret_cast<const _Float16*>(wpk), wsc, bp, mbias, npat, rcos, rsin, q_scale, groups,
                      total, x3_range_ptr());

@@ -357,6 +357,7 @@ bool launch_c(hipStream_t s, const View& x, const View& out, const AttnGeom& g, 
     groups = (g.H * g.W + ppb - 1) / ppb;
   }
   const unsigned nblocks = (unsigned)(x.B * groups);
+  note_kernel("attn_fused_kernel<%d, %d, %d, %d>", x.C, MODE, TT, DH);
 #define L(CC)                                                                                                     \
   hipLaunchKernelGGL((attn_fused_kernel<CC, MODE, TT, DH>), dim3(nblocks), dim3(256), 0, s, x.p, out.p, x.sb, x.sc, \
                      x.st, out.sb, out.sc, g, gamma, lw, lb, wqkv, wp, bp, bias_dense, bstride, rcos, rsin, q_scale,  \

@@ -875,6 +875,8 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
   }
   constexpr bool TILE_OK = C == 64 && NW == 8;
   auto kern = tile ? &attn_x3_kernel<C, MODE, DH, NW, TILE_OK, BF> : &attn_x3_kernel<C, MODE, DH, NW, false, BF>;
+  note_kernel("attn_x3_kernel<%d, %d, %d, %d, %s, %s>", C, MODE, DH, NW, tile && TILE_OK ? "true" : "false",
+              BF ? "true" : "false");
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, s, x.p, out.p, x.sb, x.sc, x.st, out.sb, out.sc, g, gamma,
                      lw, lb, reinterpret_cast<const _Float16*>(wpk), wsc, bp, mbias, npat, rcos, rsin, q_scale, groups,
                      total, x3_range_ptr(), dbg, ts);

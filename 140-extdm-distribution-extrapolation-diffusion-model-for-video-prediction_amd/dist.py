@@ -5,8 +5,8 @@ eval BatchNorm, per-sample quantile, attention within a sample), so the global
 '(b n)' batch is split into contiguous slices, one process per GPU, with no
 collective on the data path; the noise stream is keyed by the global sample
 index (`sample_base` = the slice start), so results do not depend on the rank
-count. The one exchange step is the final all-gather of the generated videos
-(RCCL over xGMI when the backend is "nccl").
+count. The one exchange step is the final gather of the generated videos to rank 0
+(RCCL point-to-point over xGMI when the backend is "nccl").
 """
 import os
 
@@ -34,18 +34,28 @@ def _host_staged():
     return dist.is_initialized() and dist.get_backend() == 'gloo'
 
 
-def gather_shards(local, global_batch, world):
-    """All-gather the ranks' slices (dim 0) into the global batch in rank order.
-    Uneven slices are padded to the largest one for the collective."""
-    if world == 1:
+def gather_shards(local, global_batch, world, dst=0):
+    """Gather the ranks' slices (dim 0) into the global batch, in rank order, on rank `dst` only
+    (the eval driver's consumer: the other ranks return None). Uneven slices are padded to the
+    largest one for the collective. Over nccl (RCCL) the device tensors go straight into
+    `dist.gather` (point-to-point xGMI transfers into dst: (world - 1) x cap x frame bytes arrive
+    at dst, nothing at the others); over gloo they are staged through host memory. Without a
+    process group (world 1) the local slice is the batch."""
+    if not dist.is_initialized():
+        assert world == 1, 'gather_shards: world > 1 without a process group'
         return local
+    world = dist.get_world_size()
+    rank = dist.get_rank()
     if _host_staged() and local.device.type != 'cpu':
-        return gather_shards(local.cpu(), global_batch, world).to(local.device)
+        out = gather_shards(local.cpu(), global_batch, world, dst)
+        return None if out is None else out.to(local.device)
     cap = -(-global_batch // world)
     pad = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[:local.shape[0]] = local
-    parts = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(parts, pad)
+    parts = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+    dist.gather(pad, parts, dst=dst)
+    if rank != dst:
+        return None
     out = []
     for r in range(world):
         _, n = shard(global_batch, world, r)
@@ -54,8 +64,9 @@ def gather_shards(local, global_batch, world):
 
 
 def max_over_ranks(value, device=None):
-    """The slowest rank's wall time (bench.py's timing rule)."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    """The slowest rank's wall time (bench.py's timing rule); over nccl the reduction runs on
+    `device` (a one-element RCCL all-reduce)."""
+    if not dist.is_initialized():
         return value
     t = torch.tensor([value], dtype=torch.float64, device=None if _host_staged() else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -308,7 +308,10 @@ class FlowDiffusion(nn.Module):
             # tc - 1 early maps and ONE resize of the repeated reference map per output frame
             # (a frame stride of 0), written straight into the [B, C, tc - 1 + tp, fs, fs] tensor
             fs = ret['real_vid_grid'].shape[-1]
-            early_t = early.permute(1, 2, 0, 3, 4)  # [B, C, tc - 1, h, w]
+            # (fp32 with contiguous H x W planes, as the kernel takes them: a no-op for the
+            # native generator's output, a conversion for an fp16 / channels-last bottleneck)
+            early_t = early.permute(1, 2, 0, 3, 4).float().contiguous()  # [B, C, tc - 1, h, w]
+            ref_fea = ref_fea.float().contiguous()
             fea = _lib.bilinear_frames(early_t if tc > 1 else None, ref_fea.unsqueeze(2).expand(-1, -1, tp, -1, -1),
                                        tc - 1, tc - 1 + tp, (fs, fs))
         else:

@@ -115,8 +115,12 @@ class Unet3D(nn.Module):
     # reuse their handles instead of re-packing every weight on each switch
     _NATIVE_CACHE = 4
 
-    def native(self, timesteps_buffers, max_batch, device_index):
-        ver = (self._state_version(), id(timesteps_buffers), max_batch, device_index, self.precision,
+    def native(self, timesteps_buffers, max_batch, device_index, precision=None):
+        """The library handle for this state / schedule / batch / device; `precision` overrides
+        self.precision for this call only (GaussianDiffusion's FP32 fallback) without changing
+        the module, so other users of the denoiser keep its own precision."""
+        precision = precision or self.precision
+        ver = (self._state_version(), id(timesteps_buffers), max_batch, device_index, precision,
                self.ucfg.fea_size)
         cache = self.__dict__.setdefault('_natives', {})
         h = cache.get(ver)
@@ -129,7 +133,7 @@ class Unet3D(nn.Module):
             while len(cache) >= self._NATIVE_CACHE:
                 del cache[next(iter(cache))]
             h = _lib.Handle(self.ucfg, int(timesteps_buffers['betas'].shape[0]), max_batch, device_index,
-                            precision=self.precision)
+                            precision=precision)
             sd = {k: v for k, v in self.state_dict().items()}
             sd.update(timesteps_buffers)
             h.load_state(sd)
@@ -137,6 +141,13 @@ class Unet3D(nn.Module):
             cache[ver] = h
         self._native, self._native_version = h, ver
         return h
+
+    def range_flag(self, reset=True):
+        """The f16x3 range flag of the denoiser's last native handle (nonzero: an operand split
+        since the last reset reached |v| >= 65504, include/extdm.h extdm_range_flag); 0 before
+        any native call."""
+        h = getattr(self, '_native', None)
+        return 0 if h is None else h.range_flag(reset)
 
     def _sched(self):
         sch = getattr(self, '_sched_buffers', None)
@@ -266,7 +277,8 @@ class GaussianDiffusion(nn.Module):
             self._bufs_cache = bufs
         self.denoise_fn._sched_buffers = self._bufs_cache
         self.denoise_fn.max_batch = max(B, self.max_batch)
-        return self.denoise_fn.native(self._bufs_cache, max(B, self.max_batch), device.index or 0)
+        return self.denoise_fn.native(self._bufs_cache, max(B, self.max_batch), device.index or 0,
+                                      precision='fp32' if getattr(self, '_fp32_fallback', False) else None)
 
     def _seed(self):
         # drawn from torch's default generator so torch.manual_seed makes runs reproducible
@@ -279,19 +291,21 @@ class GaussianDiffusion(nn.Module):
         fp16 range (|v| >= 65504) makes the library reject the sampling call (runtime.cpp
         extdm_sample); the call is then re-run on an FP32 handle (the exact fp32-MFMA kernels)
         and the denoiser stays on FP32 from then on (a checkpoint that trips the guard once
-        keeps tripping it), logged once."""
+        keeps tripping it), logged once. The fallback is this GaussianDiffusion's state (passed to
+        Unet3D.native as a per-call precision): the shared Unet3D module keeps its own precision,
+        so other wrappers and direct Unet3D.forward calls on it are unaffected. The guard covers
+        the sampling loop (sample / p_sample_loop / ddim_sample); a direct Unet3D.forward or a
+        single p_sample call on an out-of-range input returns the f16x3 result unchecked —
+        Unet3D.range_flag() reads the flag after such a call."""
         fn = self.denoise_fn
-        if getattr(self, '_fp32_fallback', False) and fn.precision != 'fp32':
-            fn.precision = 'fp32'
         try:
             return run(self._native(B, device, fea_size))
         except RuntimeError as e:
-            if self._RANGE_MSG not in str(e) or fn.precision == 'fp32':
+            if self._RANGE_MSG not in str(e) or getattr(self, '_fp32_fallback', False) or fn.precision == 'fp32':
                 raise
             warnings.warn('ExtDM: f16x3 activations reached the fp16 range (|v| >= 65504); re-running '
                           'the sampling call and continuing on the FP32 kernels', RuntimeWarning)
             self._fp32_fallback = True
-            fn.precision = 'fp32'
             return run(self._native(B, device, fea_size))
 
     @torch.inference_mode()

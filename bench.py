@@ -61,7 +61,55 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 matrix peak
 # f16x3: three v_mfma_f32_32x32x16_f16 per fp32 product; fp16 dense MFMA peak 2516.6 TF/s
 # (32x32x16 = 32768 FLOP per 32 cycles per SIMD, 1024 SIMDs, 2.4 GHz) / 3
 F16X3_PEAK_TFLOPS = 2516.6 / 3
+BF16_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA (v_mfma_f32_32x32x16_bf16), same rate as fp16
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E peak
+PEAKS = {'fp32': FP32_MFMA_PEAK_TFLOPS, 'f16x3': F16X3_PEAK_TFLOPS, 'bf16': BF16_PEAK_TFLOPS}
+# kernel families by the arithmetic their MFMAs run (template arguments decide where listed in
+# kernel_arith): fp32 MFMA kernels, and the f16x3 ones
+FP32_FAMILIES = ('attn_fused_kernel', 'window_attn_kernel', 'cross_attn_kernel', 'conv_kernel', 'conv_halo_kernel',
+                 'conv_gemm_kernel')
+X3_FAMILIES = ('conv_x3_kernel', 'conv_gemm_x3_kernel', 'xpath_x3_kernel', 'noise_pool_x3_kernel',
+               'cross_attn_x3_kernel', 'cross_attn_x3p_kernel', 'fea_side_x3_kernel', 'pw_x3_kernel')
+
+
+def _template(kname):
+    """('ident', [template args]) of 'ident<a, b, ...>' (args [] without a template list)."""
+    base = kname.split(' (')[0].strip()
+    if '<' not in base:
+        return base, []
+    ident, rest = base.split('<', 1)
+    return ident.strip(), [a.strip() for a in rest.rsplit('>', 1)[0].split(',')]
+
+
+def kernel_arith(kname, precision):
+    """The arithmetic of a launched kernel, from its template: 'fp32' (fp32 MFMA), 'f16x3' (three
+    fp16 MFMAs per fp32 product), 'bf16', or 'f16x3+bf16' (the fused attention kernels in
+    BF16_ATTN: qkv / proj on f16x3, QK^T / PV on bf16).
+      attn_core_kernel<MODE, X3, NT>         X3 true: f16x3, false: bf16
+      attn_x3_kernel<C, MODE, DH, NW, TILE, BF>, stw64_x3_kernel<C, DH, NW, BF>
+                                             BF false: f16x3, true: f16x3+bf16
+    Other families by name (FP32_FAMILIES / X3_FAMILIES); unknown names by the handle's precision."""
+    ident, args = _template(kname)
+    if ident == 'attn_core_kernel' and len(args) == 3:
+        return 'f16x3' if args[1] == 'true' else 'bf16'
+    if ident == 'attn_x3_kernel' and len(args) == 6:
+        return 'f16x3+bf16' if args[5] == 'true' else 'f16x3'
+    if ident == 'stw64_x3_kernel' and len(args) == 4:
+        return 'f16x3+bf16' if args[3] == 'true' else 'f16x3'
+    if ident in FP32_FAMILIES:
+        return 'fp32'
+    if ident in X3_FAMILIES:
+        return 'f16x3'
+    return 'fp32' if precision == 'fp32' else 'f16x3'
+
+
+def kernel_peak(arith, core_frac=0.0):
+    """Dense MFMA peak (TFLOP/s) for that arithmetic. 'f16x3+bf16': the FLOP-weighted harmonic
+    mean of the f16x3 and bf16 peaks (the time the work takes at peak), core_frac = the share of
+    the FLOPs in the bf16 QK^T / PV contractions."""
+    if arith == 'f16x3+bf16':
+        return 1.0 / ((1.0 - core_frac) / F16X3_PEAK_TFLOPS + core_frac / BF16_PEAK_TFLOPS)
+    return PEAKS[arith]
 
 
 # BASELINE.json configs as bench workloads (SURVEY §8(d) table; tc / tp per round, rounds =
@@ -73,20 +121,20 @@ WORKLOADS = {
                  precision=None, baseline='configs[1]: BAIR 64x64 ch3, cond=2 pred=14, DDPM 1000 steps, 1xMI355X'),
     'kth': dict(image=64, tc=10, tp=20, total_pred=40, sampling_steps=100, timesteps=1000, batch=16, occ=False,
                 precision=None, cpu_steady=2, baseline='configs[2]: KTH 64x64 ch1, cond=10 pred=40, DDIM 100 steps, batch=64 on 4 GPUs',
-                lead=(6, 'attn_fused_kernel<64, 0, 2, 16>', 'level-0 STW attention (ada 4x4x4 windows, dim_head 16, fp32 fused)')),
+                lead=(6, 'level-0 shifted STW attention (ada 4x4x4 windows, dim_head 16), fused LN/qkv/RoPE/softmax/PV/proj')),
     'cityscapes': dict(image=128, tc=2, tp=5, total_pred=28, sampling_steps=1000, timesteps=1000, batch=8, occ=True,
                        precision=None, cpu_steady=2, baseline='configs[3]: Cityscapes 128x128 ch3, cond=2 pred=28, DDPM 1000 steps',
-                       lead=(6, 'attn_core_kernel<0, true, 2>', 'level-0 STW attention layer (channel LN, f16x3 qkv / proj 1x1, f16x3 core over 64-token windows)')),
+                       lead=(6, 'level-0 shifted STW attention (ada_u22 4x4x4 windows, dim_head 32), fused LN/qkv/RoPE/softmax/PV/proj')),
     'ucf': dict(image=256, tc=4, tp=12, total_pred=12, sampling_steps=10, timesteps=1000, batch=4, occ=True,
                 precision='bf16_attn', cpu_steady=1, cpu_steps_max=1, baseline='configs[4]: UCF-101 256x256 ch3, cond=4 pred=12, bf16 MFMA attention',
-                lead=(6, 'attn_core_kernel<0, false, 2>', 'level-0 STW attention layer (bf16 core over 64-token windows)')),
+                lead=(6, 'level-0 shifted STW attention (ada_u22 4x4x4 windows), fused, bf16 QK^T / PV')),
     'smmnist': dict(image=64, tc=10, tp=10, total_pred=10, sampling_steps=100, timesteps=100, batch=64, occ=True,
                     precision=None, baseline='configs[0]: SMMNIST 64x64 ch1, cond=10 pred=10, DDPM 100 steps',
-                    lead=(6, 'attn_x3_kernel<64, 0, 32, 8, false>', 'level-0 STW attention (C 64, fused LN/qkv/proj, f16x3)')),
+                    lead=(6, 'level-0 shifted STW attention (C 64, 2x4x4 windows), fused LN/qkv/proj')),
 }
-# `lead`: the bench_layer id (and its launched template) of the workload's kernel with the largest
-# share of GPU time in its own DDIM-20 profile (profiles/r04_cfgprof_<config>_kernel_stats.csv);
-# it heads that config's roofline. BAIR's is LAYERS[0].
+# `lead`: the bench_layer id of the workload's kernel with the largest share of GPU time in its own
+# DDIM-20 profile (profiles/r0N_cfgprof_<config>_kernel_stats.csv); it heads that config's roofline.
+# The launched template is read back from the library (extdm_bench_layer_kernel). BAIR's is LAYERS[0].
 
 
 def parse(argv=None):
@@ -232,33 +280,30 @@ class NativeWorkload:
                                    f'decoder, occlusion map {"on" if w["occ"] else "off (eval default)"}',
                        'baseline_config': w['baseline'], 'bench_config': a.config,
                        'global_batch': self.world * B, 'batch_per_gpu': B, 'sampling_steps': a.sampling_steps,
-                       'rounds': self.rounds, 'parallelism': f'clip-shard x{self.world} (+all-gather)',
+                       'rounds': self.rounds, 'parallelism': f'clip-shard x{self.world} (+gather to rank 0)',
                        'workspace_gb': round(self.h.workspace_bytes() / 2 ** 30, 2)}}
 
-    # extdm_bench_layer ids (runtime.cpp) of the kernels reported, dominant first: the kernel
-    # with the largest share of a step's GPU time, init_conv's cond_fea branch (256 -> 64,
-    # 7x7, one ~4 ms launch per step: 15 % of the DDIM-20 profile's kernel time,
-    # profiles/r03_b64_ddim20_kernel_stats.csv), then the level-0 ResnetBlock 3x3 conv (64 ->
-    # 64 at the latent size; block1's conv stages an fp32 input, block2's copies block1's
-    # pre-split operand, id 5), the level-0 1x1 res_conv (128 -> 64, HBM-bound: 3
-    # FLOP-equivalents of f16x3 MFMA per 4-B element moved is far below the machine balance),
-    # the attention launches: level-0 shifted-window attention (6), the temporal attention (7)
-    # and TrajWarp's cross-attention core (8), and the x-branch's low-K gathers (9, 10).
-    # `kernel`: the launched template; the PMC traffic of profiles/pmc_layer<id>.json counts
-    # only when it names this template and was measured on this exact library build
-    # (lib_sha16).
-    FP32_KERNELS = ('attn_fused_kernel', 'attn_core_kernel')
+    # extdm_bench_layer ids (runtime.cpp) of the kernels reported for BAIR, dominant first: the
+    # kernel with the largest share of a step's GPU time (the phase-composed cond_fea conv), its edge
+    # corrections, the level-0 ResnetBlock 3x3 convs (block1 stages an fp32 input, block2 (5) copies
+    # block1's pre-split operand), the level-0 attention launches: shifted-window attention (6), the
+    # temporal attention (7) and TrajWarp's cross-attention core (8), the level-0 1x1 res_conv
+    # (HBM-bound: 3 FLOP-equivalents of f16x3 MFMA per 4-B element moved is far below the machine
+    # balance), the x-branch's low-K gathers (9, 10), TrajWarp's linear (12) and the level-2
+    # Tmodulator (13). `kernel`: the launched template (the attention layers' is read back from the
+    # library: extdm_bench_layer_kernel); the PMC traffic of profiles/pmc_layer<id>.json counts only
+    # when it names this template and was measured on this exact library build (lib_sha16).
     LAYERS = [(0, 'mfma', 'conv_x3_kernel<5, 1, 128, 256, 1, 4, 8, 2, true, 1, false, false, 0, true, false>',
                'init_conv cond_fea branch, phase-composed: 2 row parities x 2 column phases x 64 rows, 1x5x5 over the 16x16 map, 256 ch'),
               (11, 'mfma', 'fea_side_x3_kernel',
                'init_conv cond_fea branch edge corrections (2 line launches K = 5 x 256, 512 rows + corners)'),
               (1, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0, false, false>',
                'level-0 ResnetBlock block1 conv 64->64 1x3x3, fp32 input staged'),
-              (6, 'mfma', 'attn_x3_kernel<64, 0, 32, 8, true>',
+              (6, 'mfma', None,
                'level-0 shifted-window attention (STW, C 64, 2x4x4 windows, 8 heads x 32), fused LN/qkv/proj'),
               (5, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true, false, 0, false, false>',
                'level-0 ResnetBlock block2 conv 64->64 1x3x3, pre-split operand by LDS-DMA'),
-              (7, 'mfma', 'attn_x3_kernel<64, 1, 32, 8, true>', 'init_temporal_attn (C 64, 16 frames, 8 heads x 32), x tile by LDS-DMA'),
+              (7, 'mfma', None, 'init_temporal_attn (C 64, 16 frames, 8 heads x 32)'),
               (8, 'mfma', 'cross_attn_x3p_kernel<1>', 'TrajWarp cross-attention core (3584 queries x 512 keys, 8 heads)'),
               (4, 'hbm', 'conv_x3_kernel<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, false, 0, false, false>',
                'level-0 res_conv 128->64 1x1x1'),
@@ -268,22 +313,38 @@ class NativeWorkload:
                'TrajWarp linear_q 256->256 1x1 + ReLU, weights register-resident (pw_x3)'),
               (13, 'mfma', 'conv_x3_kernel<1, 1, 256, 256, 2, 2, 8, 2, true, 1, false, false, 0, false, false>',
                'level-2 MotionAdaptor Tmodulator, 1x1 over (T C) = 3584 -> 3584 channels of 8x8 px')]
+    # the unfused core route's other launches, reported beside layer 6 / 7 when that route is taken
+    CORE_SPLIT = {6: [(14, 'the level-0 STW layer\'s qkv 1x1 conv'), (15, 'its proj 1x1 conv + residual')],
+                  7: [(16, 'init_temporal_attn\'s qkv 1x1 conv'), (17, 'its to_out 1x1 conv + residual')]}
     # Layers whose HBM reads are whole-line coalesced streams (every wave instruction reads >= 256
     # contiguous bytes: buffer loads of 64 consecutive pixels, 1-KB LDS-DMA pieces): their PMC
-    # FETCH_SIZE gets the gfx950 x2 correction (MI355X_MICROARCH.md HBM), calibrated here on
-    # pw_x3 (layer 12), which reads each of its 234.9 MB of input exactly once: raw FETCH 118.8 MB
-    # (0.506x). Not doubled (reported raw, uncalibrated): the x-branch gathers (9, 10: overlapping
-    # per-lane 32-B windows) and the temporal attention (7: 16-B pieces four pixels wide, one
-    # frame apart; raw 287.6 MB against 268 MB of x).
-    WIDE_READS = {0, 1, 4, 5, 6, 8, 11, 12, 13}
+    # FETCH_SIZE gets the gfx950 x2 correction (MI355X_MICROARCH.md HBM), calibrated on pw_x3 (layer
+    # 12), which reads each of its 234.9 MB of input exactly once: raw FETCH 118.8 MB (0.506x). Not
+    # doubled (reported raw, uncalibrated): the x-branch gathers (9, 10: overlapping per-lane 32-B
+    # windows), the temporal attention (7: 16-B pieces four pixels wide, one frame apart) and the
+    # per-lane attention kernels (stw64_x3, attn_x3 without its tile path: 4-B loads per lane).
+    WIDE_READS = {0, 1, 4, 5, 8, 11, 12, 13}
     # HBM-bound entries: (input + output channels, spatial size per frame, frames) of the algorithmic bytes
     HBM_BYTES = {4: lambda u, T: (128 + 64, u.latent ** 2, T),
                  12: lambda u, T: (256 + 256, u.fea_size ** 2, u.tp)}
 
+    @staticmethod
+    def wide_reads(layer, kname):
+        if layer == 6:  # the STW tile path stages x by 1-KB LDS-DMA pieces
+            ident, args = _template(kname)
+            return ident == 'attn_x3_kernel' and len(args) == 6 and args[4] == 'true'
+        return layer in NativeWorkload.WIDE_READS
+
+    def pmc_path(self, layer):
+        """profiles/pmc_layer<id>.json (BAIR) or profiles/pmc_<config>_layer<id>.json."""
+        c = self.args.config
+        return os.path.join(REPO, 'profiles', f'pmc_layer{layer}.json' if c == 'bair' else f'pmc_{c}_layer{layer}.json')
+
     def _traffic(self, layer, kname):
         """HBM bytes per launch from the committed PMC passes (scripts_gpu/pmc_layers.sh), only
-        when they were taken on this library build and name the launched template."""
-        pmc = os.path.join(REPO, 'profiles', f'pmc_layer{layer}.json')
+        when they were taken on this library build, config batch and precision and name the
+        launched template."""
+        pmc = self.pmc_path(layer)
         try:
             j = json.load(open(pmc))
         except (ValueError, OSError):
@@ -292,7 +353,7 @@ class NativeWorkload:
             return None, 'PMC batch / precision differ'
         if j.get('lib_sha16') != lib_sha16():
             return None, 'PMC taken on another library build (stale)'
-        if kname not in j.get('kernel_name', ''):
+        if not kname or kname not in j.get('kernel_name', ''):
             return None, 'PMC kernel signature differs'
         if 'fetch_rule' not in j:
             return None, 'PMC file predates the raw / corrected FETCH split'
@@ -300,46 +361,79 @@ class NativeWorkload:
                f"{j['fetch_rule']}; WRITE {j['write_bytes_per_launch']} B")
         return j.get('hbm_bytes_per_launch'), src
 
+    def attn_core_frac(self, layer):
+        """Share of an attention layer's FLOPs in QK^T / PV: per token 4 N hid of 2 C 3 hid + 4 N hid
+        + 2 hid C (N = window tokens at level 0, or frames) = 4 N / (8 C + 4 N)."""
+        u = self.fd.unet.ucfg
+        T = self.tc + self.tp
+        C = u.dim
+        if layer in (6, 14, 15):
+            ws = list(u.window)
+            ext = [T, u.latent, u.latent]
+            N = 1
+            for w, e in zip(ws, ext):
+                N *= min(w, e)
+        else:
+            N = T
+        return 4.0 * N / (8.0 * C + 4.0 * N)
+
+    def layer_ids(self):
+        """(id, bound, static template or None, what) in report order: this workload's lead first."""
+        layers = list(self.LAYERS)
+        lead = self.w.get('lead')
+        if lead:
+            i = next(k for k, e in enumerate(layers) if e[0] == lead[0])
+            layers = [(lead[0], layers[i][1], None, lead[1])] + layers[:i] + layers[i + 1:]
+        return layers
+
     def roofline(self):
-        """Per kernel, timed over 20 launches of the exact forward launch with HIP events
-        on the handle's stream (extdm_bench_layer). MFMA-bound: FLOP per launch / time
-        against the f16x3 peak (dense fp16 MFMA / 3). HBM-bound: algorithmic bytes per
-        launch (fp32 input + output elements, 4 B each, weights aside) / time against
-        8 TB/s. The first entry is the dominant kernel; the others ride along."""
+        """Per kernel, timed over 20 launches of the exact forward launch with HIP events on the
+        handle's stream (extdm_bench_layer). MFMA-bound: FLOP per launch / time against the dense
+        MFMA peak of the arithmetic that kernel runs (kernel_arith: its template; f16x3 = dense fp16
+        / 3, bf16 = dense bf16, fp32 = dense fp32, f16x3+bf16 the FLOP-weighted mix). HBM-bound:
+        algorithmic bytes per launch (fp32 input + output elements, 4 B each, weights aside) / time
+        against 8 TB/s. The first entry is the dominant kernel; the others ride along."""
         B = self.args.batch
-        peak = FP32_MFMA_PEAK_TFLOPS if self.precision == 'fp32' else F16X3_PEAK_TFLOPS
         u = self.fd.unet.ucfg
         T = self.tc + self.tp
         out = []
-        layers = list(self.LAYERS)
-        lead = self.w.get('lead')
-        if lead:  # this workload's own dominant kernel first (its template name for the PMC match)
-            i = next(k for k, e in enumerate(layers) if e[0] == lead[0])
-            layers = [(lead[0], layers[i][1], lead[1], lead[2])] + layers[:i] + layers[i + 1:]
-        for layer, bound, kname, what in layers:
+        todo = list(self.layer_ids())
+        while todo:
+            layer, bound, kname, what = todo.pop(0)
             if layer == 5 and self.precision == 'fp32':
                 continue
-            # the fp32 attention kernels (no f16x3 route at these head sizes / window shapes)
-            # compute in fp32 whatever the handle's precision: priced against the fp32 peak
-            fp32_kernel = kname.startswith(self.FP32_KERNELS)
-            kpeak = FP32_MFMA_PEAK_TFLOPS if fp32_kernel else peak
             try:
                 ms_layer, flops = self.h.bench_layer(B, layer, 20)
-            except RuntimeError:  # the layer does not exist in this denoiser variant / precision
+            except RuntimeError:  # the layer does not exist in this denoiser variant / precision / route
                 continue
+            launched = self.h.bench_layer_kernel(layer)
+            if launched:
+                kname = launched
+            if kname is None:
+                kname = ''
+            if layer in self.CORE_SPLIT and launched.startswith('attn_core_kernel'):
+                # the unfused route: this entry is the core launch alone; its convs follow
+                what = what + ' — unfused route: the attention core launch alone'
+                todo[0:0] = [(i, 'mfma', None, w) for i, w in self.CORE_SPLIT[layer]]
+            arith = kernel_arith(kname, self.precision) if kname else ('fp32' if self.precision == 'fp32' else 'f16x3')
             traffic, src = self._traffic(layer, kname)
             if bound == 'mfma':
+                frac_core = self.attn_core_frac(layer) if arith == 'f16x3+bf16' else 0.0
+                kpeak = kernel_peak(arith, frac_core)
                 achieved = flops / (ms_layer * 1e-3) / 1e12
                 e = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': round(kpeak, 1), 'unit': 'TFLOP/s',
-                     'frac': round(achieved / kpeak, 4), 'flop_per_launch': flops}
+                     'frac': round(achieved / kpeak, 4), 'flop_per_launch': flops, 'arith': arith}
+                if frac_core:
+                    e['peak_note'] = (f'f16x3 qkv/proj + bf16 QK^T/PV: {frac_core:.3f} of the FLOPs at {BF16_PEAK_TFLOPS}, '
+                                      f'the rest at {F16X3_PEAK_TFLOPS:.1f} TFLOP/s (FLOP-weighted harmonic peak)')
             else:
                 ch, hw, nt = self.HBM_BYTES[layer](u, T)
                 nbytes = 4 * B * nt * hw * ch
                 achieved = nbytes / (ms_layer * 1e-3) / 1e9
                 e = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'bytes_per_launch': nbytes}
-            e.update({'kernel': f"{kname} ({what}, {'fp32' if fp32_kernel else self.precision})", 'traffic': traffic, 'traffic_src': src,
-                      'launch_ms': round(ms_layer, 4)})
+                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'bytes_per_launch': nbytes, 'arith': arith}
+            e.update({'kernel': f"{kname or '(1x1 conv)'} ({what}, {arith})", 'layer': layer, 'traffic': traffic,
+                      'traffic_src': src, 'launch_ms': round(ms_layer, 4)})
             out.append(e)
         if not out:
             return None

@@ -126,6 +126,13 @@ int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, fl
  * input; 4 = the level-0 up ResnetBlock's 1x1 res_conv (ups.3.0.res_conv); 5 = the
  * level-0 block2 conv from block1's pre-split operand, as the F16X3 forward issues it. */
 int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out, double* flops_out);
+/* (6 / 7: the level-0 STW / init_temporal attention layer — one fused launch, or on the unfused
+ * core route the attention core alone; 14 / 15: that STW layer's qkv / proj 1x1 conv alone and
+ * 16 / 17: the temporal layer's qkv / to_out, on the core route only; 8-13: see runtime.cpp.)
+ * The kernel template the last extdm_bench_layer call of `layer` launched for the attention
+ * layers (e.g. "stw64_x3_kernel<64, 16, 8, false>"), written to buf (cap bytes, NUL-terminated;
+ * empty when not recorded). bench.py prices a layer by that kernel's arithmetic. */
+int extdm_bench_layer_kernel(ExtdmHandle* h, int layer, char* buf, int cap);
 
 /* The F16X3 activation-range flag: nonzero if an operand split since the last reset
  * had |v| >= 65504 (results computed meanwhile are not fp32-accurate): bit 0 = a conv /

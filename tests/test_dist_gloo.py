@@ -1,5 +1,5 @@
 """The N > 1 clip-shard path on CPU (gloo, world size 2 and 3): contiguous
-slices keyed by the global sample index, all-gather back in rank order, and the
+slices keyed by the global sample index, gathered back to rank 0 in rank order, and the
 max-over-ranks timing reduction. The per-sample "sampler" here is a CPU stand-in
 whose output depends only on (seed, global sample index) — the property the
 native Philox stream has (tests/test_gpu_parity.py checks that bitwise on GPU)."""
@@ -35,6 +35,8 @@ def _worker(rank, world, port, global_batch, q):
         slow = D.max_over_ranks(float(rank + 1))
         if rank == 0:
             q.put((full, slow))
+        else:
+            assert full is None  # only the destination rank materialises the batch
     finally:
         dist.destroy_process_group()
 

@@ -2,15 +2,19 @@
 attention (shifted / unshifted) and temporal attention, in both precisions. BAIR levels
 0-1 (C = 64 / 128) run the fused f16x3 kernels (stw_x3.hip) in F16X3, level 2 (C = 256)
 the unfused route with the f16x3 attention core (attn_core.hip).
-Bar: max-abs <= 2e-5 on the layer output (|out| ~ 1-4; fp32 reference drift ~1e-6)."""
+Bar: max-abs <= 6e-6 on the layer output (|out| ~ 1-4; 3x the largest measured, 1.9e-6:
+profiles/r05_parity_errors.json)."""
 import importlib
 
 import pytest
+
+from tests import parity_log
 import torch
 
 from tests.golden_inputs import CONFIGS, PKG, make_sd
 
 pytestmark = pytest.mark.gpu
+ATT_BAR = 6e-6  # f16x3 / fp32 attention layers vs the oracle (module docstring)
 pkg = importlib.import_module(PKG)
 DEV = torch.device('cuda:0')
 _H = {}
@@ -61,7 +65,7 @@ def test_attention_layer_vs_oracle(prefix, level, shifted, precision, monkeypatc
     h.attn_layer(prefix, x.to(DEV), out2, shifted=bool(shifted))
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), out2.cpu())
-    assert err <= 2e-5, err
+    parity_log.check(err, ATT_BAR)
 
 
 @pytest.mark.parametrize('prefix,level,shifted', [('downs.0.1', 0, True), ('downs.2.3', 2, False),
@@ -102,7 +106,7 @@ def test_attention_core_heads6_vs_oracle(prefix, level, shifted):
     h.attn_layer(prefix, x.to(DEV), out2, shifted=bool(shifted))
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), out2.cpu())
-    assert err <= 2e-5, err
+    parity_log.check(err, ATT_BAR)
 
 
 # 64-token windows (ada / ada_u22 4x4x4): the fused stw64_x3 route. ada_kth: dim_head 16 (two
@@ -137,11 +141,11 @@ def _w64_case(name, prefix, level, shifted, precision):
 
 @pytest.mark.parametrize('name,prefix,level,shifted', W64)
 def test_window64_attention_vs_oracle(name, prefix, level, shifted):
-    """f16x3 (fp32-faithful): the same 2e-5 bar as the <= 32-token windows."""
+    """f16x3 (fp32-faithful): the same bar as the <= 32-token windows."""
     x, out, ref = _w64_case(name, prefix, level, shifted, 'f16x3')
     err = (out - ref).abs().max().item()
     print(f'{name} {prefix} f16x3 max|err| {err:.3e}')
-    assert err <= 2e-5, err
+    parity_log.check(err, ATT_BAR)
 
 
 @pytest.mark.parametrize('name,prefix,level,shifted', W64)
@@ -152,5 +156,5 @@ def test_window64_attention_bf16_vs_oracle(name, prefix, level, shifted):
     err = (out - ref).abs().max().item()
     inc = (ref - x).abs().max().item()
     print(f'{name} {prefix} bf16_attn max|err| {err:.3e} = {err / inc:.2e} x max|increment|')
-    assert err <= 1e-2 * inc, (err, inc)
+    parity_log.check(err, 1e-2 * inc, f'bf16, max|increment| {inc:.3e}')
     assert err > 1e-7  # a different arithmetic from the fp32-faithful mode

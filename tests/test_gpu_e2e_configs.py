@@ -11,16 +11,18 @@ reference itself (tests/golden/e2e.npz, tests/golden/make_golden.py e2e(); VERDI
   * SMMNIST 10 -> 10 as two DDPM-100 rounds through VideoFlowDiffusion_multi1248 and the
     eval driver's autoregressive loop (valid.py:141-186).
 
-The reference's CPU noise stream is replayed and injected. Tolerances (max-abs): a chain
-of reverse steps 5e-4 (DDPM-5) / 2e-3 (DDIM-100: 100 thresholded steps); a sample_one_video
-round 1e-3 as the other wrapper tests; two chained rounds 2e-3 (tests/test_gpu_wrappers.py).
-BF16_ATTN is not fp32-faithful: its UCF round is held to 5e-2 on the flow grid / occlusion
-map and the decoded frames (values in [-1, 1] / [0, 1]; the eps-level contract is
-tests/test_gpu_bf16_attn.py's 5e-3 x max|eps|)."""
+The reference's CPU noise stream is replayed and injected. Tolerances (max-abs), each about 3x
+the error measured on MI355X (profiles/r05_parity_errors.json): KTH DDIM-100 3e-5 (measured
+9.4e-6), Cityscapes DDPM-5 2e-6 (4.8e-7), SMMNIST 2 x DDPM-100 4e-5 (1.2e-5), the UCF
+sample_one_video round 2e-4 in F16X3 (6.2e-5) and, BF16_ATTN not being fp32-faithful, 7e-2 there
+(2.4e-2 on the decoded frames; values in [-1, 1] / [0, 1]; the eps-level contract is
+tests/test_gpu_bf16_attn.py's 5e-3 x max|eps|); the encoder keys 1e-4 in both (2.1e-5)."""
 import importlib
 
 import numpy as np
 import pytest
+
+from tests import parity_log
 import torch
 
 from tests.golden_inputs import E2E, E2E_UCF_FULL, PKG, ddim_noise, make_lfae_sd, make_sd, unet_inputs, video_inputs
@@ -56,7 +58,8 @@ def test_kth_ddim100_chain_vs_reference():
     torch.cuda.synchronize()
     err = np.abs(out.cpu().numpy() - load('e2e.npz')['kth_ddim100']).max()
     print(f'kth ddim100 max|err| {err:.2e}')
-    assert err <= 2e-3, err
+    # 3.2x the measured 9.4e-6 (profiles/r05_parity_errors.json)
+    parity_log.check(err, 3e-5)
 
 
 def test_cityscapes_ddpm5_full_size_vs_reference():
@@ -73,7 +76,8 @@ def test_cityscapes_ddpm5_full_size_vs_reference():
     torch.cuda.synchronize()
     err = np.abs(out.cpu().numpy() - load('e2e.npz')['city_ddpm5']).max()
     print(f'cityscapes ddpm5 max|err| {err:.2e}')
-    assert err <= 5e-4, err
+    # the measured 4.8e-7 x 4 (profiles/r05_parity_errors.json)
+    parity_log.check(err, 2e-6)
 
 
 def _wrapper(case, precision=None):
@@ -91,7 +95,8 @@ def _wrapper(case, precision=None):
     return fd, lc
 
 
-@pytest.mark.parametrize('precision,tol', [('f16x3', 1e-3), ('bf16_attn', 5e-2)])
+# tol ~3x the largest measured key error (profiles/r05_parity_errors.json): f16x3 6.2e-5, bf16_attn 2.4e-2
+@pytest.mark.parametrize('precision,tol', [('f16x3', 2e-4), ('bf16_attn', 7e-2)])
 def test_ucf256_sample_one_video_vs_reference(precision, tol):
     c = E2E['ucf256']
     u = c['unet']
@@ -113,8 +118,9 @@ def test_ucf256_sample_one_video_vs_reference(precision, tol):
         assert abs(float(s.sum()) - ref[0]) <= max(4 * tol * v.numel() ** 0.5, 1e-4 * ref[1]), k
     print(precision, {k: f'{v:.2e}' for k, v in errs.items()})
     # the real_* keys come from the LFAE encoder alone (fp32 in every precision mode)
-    assert max(errs['real_vid_grid'], errs['real_vid_conf']) <= 1e-3, errs
-    assert max(errs.values()) <= tol, errs
+    parity_log.check(max(errs['real_vid_grid'], errs['real_vid_conf']), 1e-4, f'{precision} encoder keys')
+    for k, v in errs.items():
+        parity_log.check(v, tol, f'{precision} {k}')
 
 
 def test_smmnist_two_ddpm100_rounds_vs_reference():
@@ -136,4 +142,5 @@ def test_smmnist_two_ddpm100_rounds_vs_reference():
     assert out.shape == g.shape
     err = np.abs(out.cpu().numpy() - g).max()
     print(f'smmnist 2 x DDPM-100 max|err| {err:.2e}')
-    assert err <= 2e-3, err
+    # 3.3x the measured 1.2e-5 (profiles/r05_parity_errors.json)
+    parity_log.check(err, 4e-5)

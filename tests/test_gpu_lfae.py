@@ -10,6 +10,8 @@ import importlib
 
 import numpy as np
 import pytest
+
+from tests import parity_log
 import torch
 
 from tests.golden_inputs import (FD_UNET, LFAE_CFG, PKG, lfae_config_dict, make_lfae_sd, make_sd, video_inputs)
@@ -36,7 +38,7 @@ def fdiff(occ):
 
 def close(a, g, tol, name):
     err = np.abs(a.detach().cpu().numpy() - g).max()
-    assert err <= tol, (name, err)
+    parity_log.check(err, tol, str(name))
 
 
 def test_region_bg_bottleneck():
@@ -91,7 +93,8 @@ def test_sample_one_video_vs_reference(occ):
     keys = sorted(k[len(f'sov_{tag}_'):] for k in g.files if k.startswith(f'sov_{tag}_'))
     assert sorted(ret) == keys
     for k in keys:
-        close(ret[k], g[f'sov_{tag}_{k}'], 1e-3, k)
+        # 1.2e-4: 3x the largest measured key error (4.0e-5, sample_warped_vid; profiles/r05_parity_errors.json)
+        close(ret[k], g[f'sov_{tag}_{k}'], 1.2e-4, k)
 
 
 def test_autoregressive_driver_rounds_and_sharding():

@@ -13,6 +13,8 @@ import importlib
 
 import numpy as np
 import pytest
+
+from tests import parity_log
 import torch
 
 from tests.golden_inputs import CONFIGS, PKG, VARIANTS, GOLDEN_BATCH, make_sd, unet_inputs
@@ -58,7 +60,7 @@ def test_unet_vs_reference_golden_both_precisions(name, precision):
     g = load(f'unet_{name}.npz')['eps']
     err = np.abs(eps.numpy() - g).max()
     bar = 1e-4 if name in ('small', 'bair') else 2e-4
-    assert err <= bar, err
+    parity_log.check(err, bar)
 
 
 def _fp64_eps(cfg, x, t, cond, fea, sd=None):
@@ -169,7 +171,8 @@ def test_f16x3_ddpm10_and_ddim10_chains_vs_reference_golden():
                noise=noises.to(DEV).contiguous())
     torch.cuda.synchronize()
     err = np.abs(out.cpu().numpy() - g['ddpm10']).max()
-    assert err <= 2e-4, err
+    # DDPM-10 4.1e-6 / DDIM-10 9.2e-6 measured (profiles/r05_parity_errors.json)
+    parity_log.check(err, 3e-5)
 
     h = handle('small', 'f16x3')
     pairs = pkg.ddim_time_pairs(1000, 10)
@@ -181,7 +184,8 @@ def test_f16x3_ddpm10_and_ddim10_chains_vs_reference_golden():
              noise=noises.to(DEV).contiguous())
     torch.cuda.synchronize()
     err = np.abs(out.cpu().numpy() - g['ddim10']).max()
-    assert err <= 2e-4, err
+    # DDPM-10 4.1e-6 / DDIM-10 9.2e-6 measured (profiles/r05_parity_errors.json)
+    parity_log.check(err, 3e-5)
 
 
 def test_f16x3_range_guard_trips():

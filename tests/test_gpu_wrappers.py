@@ -17,6 +17,8 @@ import importlib
 
 import numpy as np
 import pytest
+
+from tests import parity_log
 import torch
 
 from tests.golden_inputs import (AR_CASE, LFAE_CFG, PKG, WRAP_CASES, ddim_noise, ddpm100_case, lfae_config_dict,
@@ -57,7 +59,8 @@ def test_wrapper_sample_one_video_vs_reference(tag):
     assert sorted(ret) == keys
     for k in keys:
         err = np.abs(ret[k].cpu().numpy() - g[f'{tag}_{k}']).max()
-        assert err <= 1e-3, (k, err)
+        # 3.1x the largest measured key error (8.0e-5, u22 sample_warped_vid; profiles/r05_parity_errors.json)
+        parity_log.check(err, 2.5e-4, str(k))
 
 
 def test_u22_wrapper_needs_occlusion_like_the_reference():
@@ -93,7 +96,8 @@ def test_autoregressive_two_rounds_vs_reference():
     g = load('wrappers.npz')['ar_result']
     assert out.shape == g.shape
     err = np.abs(out.cpu().numpy() - g).max()
-    assert err <= 2e-3, err
+    # 3x the measured 8.9e-5 (profiles/r05_parity_errors.json)
+    parity_log.check(err, 2.7e-4)
 
 
 def test_ddpm100_chain_vs_reference():
@@ -114,7 +118,8 @@ def test_ddpm100_chain_vs_reference():
              noise=noises.to(DEV).contiguous(), use_graph=True)
     torch.cuda.synchronize()
     err = np.abs(out.cpu().numpy() - g['ddpm100']).max()
-    assert err <= 5e-4, err
+    # 3.6x the measured 4.1e-6 (profiles/r05_parity_errors.json)
+    parity_log.check(err, 1.5e-5)
 
 
 def test_bilinear_frames_matches_interpolate():
