@@ -32,6 +32,7 @@
 // 2^(e_q + e_k) (stw_x3.hip operand-scale note). A lane reads its query's row: 4 x 16-B
 // pieces per key tile and head.
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 
 #include "attn_x3_ops.h"
@@ -53,7 +54,17 @@ struct UL64 {
   static constexpr int HALVES = 3 * KS * FRAG + (C / 32) * 2 * FRAG;
 };
 
-template <int C, int DH, int NW, bool BF>
+// TILE (host check stw64_tile_ok; C = 64 on 8 waves): the workgroup's NW / 2 windows are consecutive
+// along W (one (wd, wh) window row, W a multiple of 16, no H / W padding), so together they cover
+// C x 4 frames x 4 rows x 16 columns of x. That block is staged once into LDS by coalesced 8-B
+// loads per lane (each 64-B row segment read by 8 adjacent lanes; a shifted row wraps only between
+// 8-B pieces), the lanes read their token's channels from it (row stride 20, channel stride 324
+// floats: the 32 tokens of a half-wave hit 32 banks, the two halves the other 32), and the epilogue
+// writes Y + bias back into it and leaves as the same 8-B pieces plus the residual — instead of
+// per-lane 4-B accesses that touch 16 lines per instruction (the per-lane prologue and epilogue
+// took 40-55 % of the kernel: EXTDM_STW64_DBG knock-outs, KTH / UCF level 0). The tile aliases the
+// K / V exchange region (used only inside the unit loop).
+template <int C, int DH, int NW, bool BF, bool TILE>
 __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, long sc, long st, AttnGeom g,
                                                            const float* __restrict__ gamma,
                                                            const _Float16* __restrict__ wpk,
@@ -63,7 +74,7 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
                                                            const float* __restrict__ rcos,
                                                            const float* __restrict__ rsin, float q_scale,
                                                            int groups_per_sample, int total_groups,
-                                                           int* __restrict__ range_flag) {
+                                                           int* __restrict__ range_flag, int dbg) {
   using UL = UL64<C>;
   constexpr int KS = UL::KS;
   constexpr int UNITS = 8 * DH / 32;  // heads 8
@@ -84,6 +95,14 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
   const int b = active ? gidx / groups_per_sample : 0;
   const int grp = active ? gidx % groups_per_sample : 0;
   float* const xb = x + (long)b * sb;
+  constexpr int WPG = NW / 2;       // windows per workgroup
+  constexpr int TC = 4 * WPG;       // tile columns
+  constexpr int TRS = TC + 4;       // tile row stride (floats)
+  constexpr int TCS = 16 * TRS + 4; // tile channel stride: 8 TCS = 32 mod 64 banks
+  constexpr int NPC = 16 * TC / 2;  // 8-B pieces per channel
+  constexpr int PPW = TILE ? C * NPC / (NW * 64) : 1;  // piece instructions per wave
+  static_assert(!TILE || (C * NPC) % (NW * 64) == 0, "tile pieces per wave");
+  float* const tileL = reinterpret_cast<float*>(wsm + 2 * UL::HALVES);
 
   // buffer descriptors: the lane's token (and channel half) in the 32-bit offset, the channel
   // row in the wave-uniform soffset, invalid tokens past the extent (host checks 31 bits)
@@ -128,6 +147,46 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
                            : 0;
   const int mb_lane = (tk * 64 + 4 * h) * 4;
   const int mb_wave = __builtin_amdgcn_readfirstlane(pat * 8 * 4096 * 4);
+  // TILE: the workgroup's first window (all its windows share (b, wd, wh)) and the lane's k-th
+  // 8-B piece: LDS float offset, global byte offset (past the extent for a padded frame)
+  const int grp0 = TILE ? (blockIdx.x * WPG) % groups_per_sample : 0;
+  const int ww0 = grp0 % nWw, wh0 = (grp0 / nWw) % nWh, wd0 = grp0 / (nWw * nWh);
+  // piece i of the lane: channel c0 + CPI i, the same (frame, row, column pair) for every i, so the
+  // offsets are a base + i x a stride (32-bit: the host checks the sample's extent < 2^30 B)
+  constexpr int CPI = NW * 64 / NPC;  // channels per wave instruction
+  static_assert(!TILE || (NW * 64) % NPC == 0, "whole channels per piece instruction");
+  struct Piece { int lbase, gbase; };
+  auto piece_base = [&](int ln) __attribute__((always_inline)) {
+    const int q = wave * 64 + ln;
+    const int c = q / NPC, rem = q % NPC, pr = rem / (TC / 2), k = rem % (TC / 2);
+    const int f = pr >> 2, r = pr & 3;
+    // (the shifted coordinates stay below twice the padded extent: a conditional subtract, not a
+    // division)
+    int gd = wd0 * 4 + f + g.ss0, gh = wh0 * 4 + r + g.ss1, gw = ww0 * 4 + 2 * k + g.ss2;
+    gd -= gd >= g.Dp ? g.Dp : 0;
+    gh -= gh >= g.Hp ? g.Hp : 0;
+    gw -= gw >= g.Wp ? g.Wp : 0;
+    Piece pc;
+    pc.lbase = c * TCS + pr * TRS + 2 * k;
+    pc.gbase = active && gd < g.D ? (c * (int)sc + gd * (int)st + gh * g.W + gw) * 4 : OOB;
+    return pc;
+  };
+  const int gstep = CPI * (int)sc * 4;  // bytes per piece index
+  auto goff_of = [&](const Piece& pc, int i) __attribute__((always_inline)) {
+    return pc.gbase == OOB ? OOB : pc.gbase + i * gstep;
+  };
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  if (TILE) {
+    u32x2 pv[PPW];
+    const Piece pc = piece_base(lane);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) pv[i] = __builtin_amdgcn_raw_buffer_load_b64(rs_x, goff_of(pc, i), 0, 0);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) *reinterpret_cast<u32x2*>(tileL + pc.lbase + i * CPI * TCS) = pv[i];
+    __syncthreads();
+  }
+  // the lane's token in the tile: frame td, row th, column 4 (window in the workgroup) + tw
+  const int tpos = ((tk >> 4) * 4 + ((tk >> 2) & 3)) * TRS + 4 * (wave >> 1) + (tk & 3);
 
   // ---- 1. channel LayerNorm into register fragments ----
   const float sq0 = wsc[0] * q_scale, sk0 = wsc[1], sv0 = wsc[2], csm = wsc[4];
@@ -142,7 +201,7 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
     for (int k = 0; k < KS; ++k)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        xv[k][e] = ldb(rs_x, vpro, (int)((16 * k + e) * sc * 4));
+        xv[k][e] = TILE ? tileL[(16 * k + 8 * h + e) * TCS + tpos] : ldb(rs_x, vpro, (int)((16 * k + e) * sc * 4));
         s += xv[k][e];
       }
     s = xh_sum(s);
@@ -203,7 +262,8 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
   const h8* const kv1 = kv0 + XS * 64;                        // and key tile 1
   constexpr int VOFF = 2 * Op<BF>::SLOTS * 64;                 // V behind K in a wave's slots
 
-  for (int u = 0; u < UNITS; ++u) {
+  // dbg (EXTDM_STW64_DBG, timing diagnostics only, results invalid): 16 = no unit loop
+  for (int u = 0; u < ((dbg & 16) ? 0 : UNITS); ++u) {
     const _Float16* W = wsm + (u & 1) * UL::HALVES;
     // unit u's slice has landed (LDS-DMA completion is per issuing wave: drain, then barrier),
     // slot (u + 1) & 1 and every wave's exchange slots of unit u - 1 are free
@@ -284,18 +344,22 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
     __syncthreads();  // both tiles' K / V are in LDS
     if (!active) continue;
 
-    f32x16 o;
+    // O^T per head: a dim-16 unit's two heads accumulate apart over the whole V (no per-lane
+    // masking of the other head's V rows: 64 v_cndmask per unit) and the epilogue takes rows
+    // 0-7 of the registers (dims 0-15: head 0) from o[0] and rows 8-15 from o[1]
+    f32x16 o[HPU];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    for (int hh = 0; hh < HPU; ++hh)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[hh][r] = 0.f;
 #pragma unroll
     for (int hh = 0; hh < HPU; ++hh) {
-      // S^T[kt] = K[kt] Q^T (rows = keys of tile kt, lane = query) from zero, then the bias /
-      // mask in one add (one rounding, as the reference's qk^T + bias)
+      // S^T[kt] = bias + K[kt] Q^T (rows = keys of tile kt, lane = query): the bias / mask rows are
+      // the chain's initial accumulator (no separate add; the chain rounds at the bias's scale)
       f32x16 sc_[2];
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sc_[kt][r] = 0.f;
+        sc_[kt] = bia[kt];
 #pragma unroll
         for (int s = 0; s < 2; ++s)
           if (HPU == 1 || s == hh) {
@@ -303,8 +367,6 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
             kf.get((kt ? kv1 : kv0) + s * Op<BF>::SLOTS * 64);
             sc_[kt] = mmo(kf, qf[s], sc_[kt]);
           }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sc_[kt][r] += bia[kt][r];
       }
       if (hh + 1 < HPU) load_bias(hh + 1);
       float mx = -INFINITY;
@@ -313,8 +375,9 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc_[kt][r]);
       mx = xh_max(mx);
-      // exp(s - mx) as v_exp_f32 of fma(s, log2 e 2^-(e_q+e_k), -mx ...): masked -inf -> 0
-      const float mxl = mx * csm;
+      // P' = 16 exp(s - mx) = v_exp_f32 of fma(s, log2 e 2^-(e_q+e_k), 4 - mx ...) (masked -inf -> 0),
+      // unnormalised: O is scaled by 16 / sum P' after PV (16 or 8 products instead of 32)
+      const float mxl = mx * csm - 4.f;
       float sum = 0.f;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -324,29 +387,31 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
           sum += sc_[kt][r];
         }
       sum = xh_sum(sum);
-      const float inv = 16.f / sum;  // P * 2^4 (stw_x3.hip operand-scale note)
-      // O^T[dd][i] += sum_j V^T[dd][j] P^T[j][i]; lanes of the unit's other head masked
-      const bool minehead = HPU == 1 || (lc / DH) == hh;
+      const float inv = 16.f / sum;  // O carries P = 16 p (stw_x3.hip operand-scale note)
+      // O^T[dd][i] += sum_j V^T[dd][j] P'^T[j][i]
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           float tp[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) tp[e] = sc_[kt][8 * s + e] * inv;
+          for (int e = 0; e < 8; ++e) tp[e] = sc_[kt][8 * s + e];
           Op<BF> pf, vf;
           pf.set(tp, bad);
           vf.get((kt ? kv1 : kv0) + VOFF + s * Op<BF>::SLOTS * 64);
-          if (!minehead) vf.zero();
-          o = mmo(vf, pf, o);
+          o[hh] = mmo(vf, pf, o[hh]);
         }
+      // the head's rows: all 16 registers (dim 32), registers 8 hh .. 8 hh + 7 (dim 16)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (HPU == 1 || (r >> 3) == hh) o[hh][r] *= inv;
     }
     // projection: Y[c][i] += sum_dd Wp[c][u*32 + dd] O^T[dd][i] (f16x3)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       float to[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) to[e] = o[8 * s + e];
+      for (int e = 0; e < 8; ++e) to[e] = o[HPU == 1 ? 0 : s][8 * s + e];
       h8 oh, ol;
       split8<false>(to, oh, ol, bad);
 #pragma unroll
@@ -367,7 +432,46 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
   }
   if (bad) atomicOr(range_flag, 2);
   // ---- 3. bias + residual, in place (row cu + 4h of register r) ----
-  if (valid) {
+  if (TILE && !(dbg & 8)) {
+    // Y + bias into the tile (its exchange alias is free once every wave is past the loop), then
+    // the tile's 8-B pieces + the residual leave as the prologue's coalesced pieces; padded
+    // frames' offsets lie past the extent (stores dropped). The sum order is the per-lane
+    // path's: (Y + bias) + x.
+    const float spj = wsc[3];
+    const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bp), 0, C * 4, 0x00020000);
+    __syncthreads();
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int cu = ct * 32 + (r & 3) + 8 * (r >> 2);
+        tileL[(cu + 4 * h) * TCS + tpos] = pacc[ct][r] * spj + ldb(rs_b, 16 * h, cu * 4);
+      }
+    __syncthreads();
+    u32x2 xr[PPW];
+    // an opaque lane id: the two offsets recomputed here rather than kept live through the unit
+    // loop from the prologue (hipcc would CSE them)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const Piece pc = piece_base(ln);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) xr[i] = __builtin_amdgcn_raw_buffer_load_b64(rs_x, goff_of(pc, i), 0, 0);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const u32x2 y = *reinterpret_cast<const u32x2*>(tileL + pc.lbase + i * CPI * TCS);
+      u32x2 o;
+      o[0] = __float_as_uint(__uint_as_float(y[0]) + __uint_as_float(xr[i][0]));
+      o[1] = __float_as_uint(__uint_as_float(y[1]) + __uint_as_float(xr[i][1]));
+      __builtin_amdgcn_raw_buffer_store_b64(o, rs_x, goff_of(pc, i), 0, 0);
+    }
+  } else if (dbg & 8) {  // timing only: no epilogue loads / stores (one store keeps the work live)
+    float acc = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc += pacc[ct][r];
+    if (acc == 12345.f) xb[pos] = acc;
+  } else if (valid) {
     const float spj = wsc[3];
     const int vex = (int)((4 * h * sc + pos) * 4);
     const auto rs_b = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bp), 0, C * 4, 0x00020000);
@@ -384,25 +488,45 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
   }
 }
 
+// The TILE path's geometry (kernel note): 4x4x4 windows without H / W padding, W a multiple of 16
+// (whole 4-window groups per window row), 8-B aligned rows; EXTDM_STW64_NO_TILE=1 forces the
+// per-lane path (A/B)
+bool stw64_tile_ok(const View& x, const AttnGeom& g, int groups) {
+  static const bool off = [] { const char* v = getenv("EXTDM_STW64_NO_TILE"); return v && v[0] && v[0] != '0'; }();
+  return !off && x.C == 64 && g.ws0 == 4 && g.ws1 == 4 && g.ws2 == 4 && g.H == g.Hp && g.W == g.Wp && g.W % 16 == 0 &&
+         groups % 4 == 0 && x.st == (long)x.H * x.W && x.sc % 2 == 0 && x.sb % 2 == 0 && x.st % 2 == 0 &&
+         ((uintptr_t)x.p & 7) == 0;
+}
+
 template <int C, int DH, int NW, bool BF>
 void launch(hipStream_t s, const View& x, const AttnGeom& g, int groups, const float* gamma, const void* wpk,
             const float* wsc, const float* bp, const float* mbias, int npat, const float* rcos, const float* rsin,
             float q_scale) {
   constexpr int XS = 2 * 2 * Op<BF>::SLOTS;
-  const size_t lds = (size_t)2 * UL64<C>::HALVES * sizeof(_Float16) + (size_t)NW * XS * 64 * 16;
+  constexpr bool TILE_OK = C == 64 && NW == 8;
+  const bool tile = TILE_OK && stw64_tile_ok(x, g, groups);
+  const size_t ring = (size_t)2 * UL64<C>::HALVES * sizeof(_Float16);
+  const size_t xch = (size_t)NW * XS * 64 * 16;
+  const size_t tileb = (size_t)C * (16 * (2 * NW + 4) + 4) * sizeof(float);  // TCS floats per channel
+  const size_t lds = ring + (tile ? std::max(xch, tileb) : xch);
   static std::once_flag once[64];
   int dev = 0;
   (void)hipGetDevice(&dev);
   std::call_once(once[dev & 63], [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stw64_x3_kernel<C, DH, NW, BF>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stw64_x3_kernel<C, DH, NW, BF, false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (TILE_OK)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&stw64_x3_kernel<C, DH, NW, BF, TILE_OK>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
   const int total = x.B * groups;
   const int grid = (total + NW / 2 - 1) / (NW / 2);
-  note_kernel("stw64_x3_kernel<%d, %d, %d, %s>", C, DH, NW, BF ? "true" : "false");
-  hipLaunchKernelGGL((stw64_x3_kernel<C, DH, NW, BF>), dim3(grid), dim3(NW * 64), lds, s, x.p, x.sb, x.sc, x.st, g,
-                     gamma, reinterpret_cast<const _Float16*>(wpk), wsc, bp, mbias, npat, rcos, rsin, q_scale, groups,
-                     total, x3_range_ptr());
+  note_kernel("stw64_x3_kernel<%d, %d, %d, %s, %s>", C, DH, NW, BF ? "true" : "false", tile ? "true" : "false");
+  static const int dbg = [] { const char* v = getenv("EXTDM_STW64_DBG"); return v ? atoi(v) : 0; }();
+  auto kern = tile ? &stw64_x3_kernel<C, DH, NW, BF, TILE_OK> : &stw64_x3_kernel<C, DH, NW, BF, false>;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, s, x.p, x.sb, x.sc, x.st, g, gamma,
+                     reinterpret_cast<const _Float16*>(wpk), wsc, bp, mbias, npat, rcos, rsin, q_scale, groups, total,
+                     x3_range_ptr(), dbg);
 }
 
 template <int DH, bool BF>

@@ -6,7 +6,7 @@ P=/root/repo/140-extdm-distribution-extrapolation-diffusion-model-for-video-pred
 F=$1; TAG=$2; K=$3
 mkdir -p /tmp/isa/$TAG && cd /tmp/isa/$TAG || exit 1
 EXTRA=""
-case $F in stw_x3.hip|cross_x3.hip) EXTRA="-fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form=1";; attn_core.hip) EXTRA="-mllvm -amdgpu-mfma-vgpr-form=1";; xpath_x3.hip) EXTRA="-fno-slp-vectorize";; esac
+case $F in stw_x3.hip|stw64_x3.hip|cross_x3.hip) EXTRA="-fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form=1";; attn_core.hip) EXTRA="-mllvm -amdgpu-mfma-vgpr-form=1";; xpath_x3.hip) EXTRA="-fno-slp-vectorize";; esac
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I /root/repo/include -I $P/csrc $EXTRA \
   --save-temps -Rpass-analysis=kernel-resource-usage -c $P/csrc/$F -o out.o 2> remarks.txt || { cat remarks.txt | grep error; exit 1; }
 S=$(ls *-hip-amdgcn-amd-amdhsa-gfx950.s)
