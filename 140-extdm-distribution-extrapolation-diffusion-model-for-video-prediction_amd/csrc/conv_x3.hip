@@ -167,8 +167,12 @@ template <> struct XMaxX3<5, 256> { static constexpr int v = 400; };
 // out-of-image position past the extent so it loads 0; or the operand by LDS-DMA) for the next
 // channel block at its first stage and waits for them at its last: STG stages of cover. The raw
 // tile is split into the [hl][c8][pos][8] operand layout by all waves between channel blocks.
+// BX: the buffer-load X staging (BUFX) known to apply at compile time (host: x3_bufx_ok). With the
+// runtime choice both staging paths shared the channel-block loop, and merging them cost the loop
+// register copies and 64-bit address arithmetic on the path taken (static count of the level-0
+// 3x3 tile's loop: 1192 VALU + 521 SALU per 108 MFMAs; 249 + 218 with BX).
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
-          bool RGN = false, int SPL = 0, bool PH = false, bool WS = false>
+          bool RGN = false, int SPL = 0, bool PH = false, bool WS = false, bool BX = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4 && KS == 5 ? 2 : 1))) void conv_x3_kernel(X3Args a) {
   constexpr int NT = NW * 64;
   constexpr int PAD = KS / 2;
@@ -273,7 +277,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   const int gC0 = a.C0, gCin = a.Cin;
   // channel groups never straddle the two sources nor run past Cin (wave-uniform)
   const bool whole = gC0 % 16 == 0 && gCin % CIB == 0;
-  const bool bufx = EXTDM_X3_BUFX && whole && a.in0_bytes > 0;
+  const bool bufx = BX || (EXTDM_X3_BUFX && whole && a.in0_bytes > 0);
   const auto rsx0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in0), 0, a.in0_bytes, 0x00020000);
   const auto rsx1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.in1), 0, a.in1_bytes, 0x00020000);
   auto load_x_exact = [&](int cgb) __attribute__((always_inline)) {
@@ -866,6 +870,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 4
   }
 }
 
+// the BX precondition: the kernel's bufx test (whole 16-channel groups in each source, extents set)
+bool x3_bufx_ok(const X3Args& a, int cib) {
+  static const bool off = [] { const char* v = getenv("EXTDM_X3_NO_BX"); return v && v[0] && v[0] != '0'; }();
+  return !off && EXTDM_X3_BUFX && a.C0 % 16 == 0 && a.Cin % cib == 0 && a.in0_bytes > 0;
+}
+
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN, int NS, bool XOP = false,
           bool RGN = false, int SPL = 0, bool PH = false, bool WS = false>
 void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
@@ -879,13 +889,27 @@ void launch_sp(hipStream_t s, const X3Args& a, unsigned ntiles) {
   // + 32 halves (unused-slot dummy) + 2 * BM floats (epilogue scale / bias)
   const size_t lds = ((size_t)2 * AH + (size_t)XB * 2 * xlo + raw + 32 + 4 * BM) * sizeof(_Float16);
   dim3 grid(ntiles, (a.Cout + BM - 1) / BM, SPL == 1 ? a.nsplit : 1);
+  // BX only where the staging loads run (not the operand-input / WS-raw / split-K-sum tiles)
+  constexpr bool BXV = !XOP && !WSR && SPL != 2 && SPAN;
+  const bool bx = BXV && x3_bufx_ok(a, 16 * NG);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH, WS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (BXV)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH, WS, BXV>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH, WS>), grid, dim3(NW * 64), lds, s, a);
+  if (SPL != 2) {
+    auto tf = [](bool v) { return v ? "true" : "false"; };
+    note_kernel("conv_x3_kernel<%d, %d, %d, %d, %d, %d, %d, %d, %s, %d, %s, %s, %d, %s, %s, %s>", KS, KY, BM, BN, NG, WN,
+                NW, XBUF, tf(SPAN), NS, tf(XOP), tf(RGN), SPL, tf(PH), tf(WS), tf(bx));
+  }
+  if (bx)
+    hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH, WS, BXV>), grid, dim3(NW * 64), lds, s, a);
+  else
+    hipLaunchKernelGGL((conv_x3_kernel<KS, KY, BM, BN, NG, WN, NW, XBUF, SPAN, NS, XOP, RGN, SPL, PH, WS>), grid, dim3(NW * 64), lds, s, a);
 }
 
 template <int KS, int KY, int BM, int BN, int NG, int WN, int NW, int XBUF, bool SPAN>

@@ -2493,7 +2493,9 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
         if (layer == 0) REQUIRE(conv_x3_phase_forward(s, r, f, w5, e, edge), "bench layer 0: phase conv rejected");
         else REQUIRE(fea_edges_forward(s, r, edge, Cf, fw.side, fw.side_scale, fw.corner), "bench layer 11: edges rejected");
       };
+      note_kernel("");
       launch();
+      h->bench_kernel[layer] = noted_kernel();
       hipEvent_t e0, e1;
       HIPCHK(hipEventCreate(&e0));
       HIPCHK(hipEventCreate(&e1));
@@ -2534,7 +2536,9 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
       }
       fill_normal(s, in.p, 1, (int)in.numel(), 17, 0, 0, 7);
       auto launch = [&, in, out] { h->conv(out, in, nullptr, w, 1, 0, h->D(bn), nullptr, layer == 12 ? ACT_RELU : ACT_NONE); };
+      note_kernel("");
       launch();
+      h->bench_kernel[layer] = noted_kernel();
       hipEvent_t e0, e1;
       HIPCHK(hipEventCreate(&e0));
       HIPCHK(hipEventCreate(&e1));
@@ -2596,7 +2600,9 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
         h->conv(r, x0, in1, w, 1, ks / 2, bias);
       }
     };
+    note_kernel("");
     launch();  // warm
+    h->bench_kernel[layer] = noted_kernel();
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));

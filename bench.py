@@ -290,28 +290,29 @@ class NativeWorkload:
     # temporal attention (7) and TrajWarp's cross-attention core (8), the level-0 1x1 res_conv
     # (HBM-bound: 3 FLOP-equivalents of f16x3 MFMA per 4-B element moved is far below the machine
     # balance), the x-branch's low-K gathers (9, 10), TrajWarp's linear (12) and the level-2
-    # Tmodulator (13). `kernel`: the launched template (the attention layers' is read back from the
-    # library: extdm_bench_layer_kernel); the PMC traffic of profiles/pmc_layer<id>.json counts only
+    # Tmodulator (13). `kernel`: the launched template (None: read back from the library,
+    # extdm_bench_layer_kernel — the attention layers' route and the conv tiles' template arguments
+    # are chosen per launch); the PMC traffic of profiles/pmc_layer<id>.json counts only
     # when it names this template and was measured on this exact library build (lib_sha16).
-    LAYERS = [(0, 'mfma', 'conv_x3_kernel<5, 1, 128, 256, 1, 4, 8, 2, true, 1, false, false, 0, true, false>',
+    LAYERS = [(0, 'mfma', None,
                'init_conv cond_fea branch, phase-composed: 2 row parities x 2 column phases x 64 rows, 1x5x5 over the 16x16 map, 256 ch'),
               (11, 'mfma', 'fea_side_x3_kernel',
                'init_conv cond_fea branch edge corrections (2 line launches K = 5 x 256, 512 rows + corners)'),
-              (1, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0, false, false>',
+              (1, 'mfma', None,
                'level-0 ResnetBlock block1 conv 64->64 1x3x3, fp32 input staged'),
               (6, 'mfma', None,
                'level-0 shifted-window attention (STW, C 64, 2x4x4 windows, 8 heads x 32), fused LN/qkv/proj'),
-              (5, 'mfma', 'conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 1, true, false, 0, false, false>',
+              (5, 'mfma', None,
                'level-0 ResnetBlock block2 conv 64->64 1x3x3, pre-split operand by LDS-DMA'),
               (7, 'mfma', None, 'init_temporal_attn (C 64, 16 frames, 8 heads x 32)'),
               (8, 'mfma', 'cross_attn_x3p_kernel<1>', 'TrajWarp cross-attention core (3584 queries x 512 keys, 8 heads)'),
-              (4, 'hbm', 'conv_x3_kernel<1, 1, 64, 128, 2, 4, 4, 2, true, 1, false, false, 0, false, false>',
+              (4, 'hbm', None,
                'level-0 res_conv 128->64 1x1x1'),
               (9, 'mfma', 'xpath_x3_kernel<2>', 'init_conv x-branch as one composed 13x13 conv 3->64, K = 3x169'),
               (10, 'mfma', 'noise_pool_x3_kernel', 'init_noise_conv 3->256 1x7x7 + MaxPool(1,2,2), K = 3x49'),
               (12, 'hbm', 'pw_x3_kernel',
                'TrajWarp linear_q 256->256 1x1 + ReLU, weights register-resident (pw_x3)'),
-              (13, 'mfma', 'conv_x3_kernel<1, 1, 256, 256, 2, 2, 8, 2, true, 1, false, false, 0, false, false>',
+              (13, 'mfma', None,
                'level-2 MotionAdaptor Tmodulator, 1x1 over (T C) = 3584 -> 3584 channels of 8x8 px')]
     # the unfused core route's other launches, reported beside layer 6 / 7 when that route is taken
     CORE_SPLIT = {6: [(14, 'the level-0 STW layer\'s qkv 1x1 conv'), (15, 'its proj 1x1 conv + residual')],

@@ -23,5 +23,7 @@ for prec in precs:
     h.bench_layer(B, layers[0], iters)  # clock ramp
     for layer in layers:
         ms, flops = h.bench_layer(B, layer, iters)
-        print(f'{prec:6s} layer {layer} B={B}: {ms * 1e3:9.1f} us/launch, {flops / ms / 1e9:7.1f} TFLOP/s', flush=True)
+        tag = os.environ.get('EXTDM_X3_NO_BX', '')
+        print(f'{prec:6s} layer {layer} B={B}: {ms * 1e3:9.1f} us/launch, {flops / ms / 1e9:7.1f} TFLOP/s '
+              f'{h.bench_layer_kernel(layer)} NO_BX={tag}', flush=True)
     del h
