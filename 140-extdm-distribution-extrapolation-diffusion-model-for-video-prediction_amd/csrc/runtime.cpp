@@ -117,6 +117,13 @@ struct ExtdmHandle {
   const bool fuse_res_gn = [] { const char* v = getenv("EXTDM_NO_RES_GN"); return !(v && v[0] && v[0] != '0'); }();
   int* t_batch = nullptr;
   int* step_ctr = nullptr;
+  unsigned* sel = nullptr;  // the multi-workgroup sampler step's selection bins (sampler_sel_bytes)
+  // the sampler step over (chunk, sample) workgroups (sampler.hip); EXTDM_SAMPLER_1WG=1 restores the
+  // one-workgroup-per-sample kernel with its set_t / incr launches (A/B)
+  static bool sampler_mw() {
+    static const bool off = [] { const char* v = getenv("EXTDM_SAMPLER_1WG"); return v && v[0] && v[0] != '0'; }();
+    return !off;
+  }
   StepCoef* coefs = nullptr;
   int coefs_cap = 0;
   float* eps_buf = nullptr;
@@ -2050,6 +2057,7 @@ struct ExtdmHandle {
     partials = reinterpret_cast<double*>(dmalloc(((size_t)B * 8 * 64 * 2 + (size_t)B * 8 + (size_t)B * 512) * sizeof(double)));
     t_batch = reinterpret_cast<int*>(dmalloc((size_t)std::max(B, 1) * sizeof(int)));
     step_ctr = reinterpret_cast<int*>(dmalloc(sizeof(int) * 4));
+    sel = reinterpret_cast<unsigned*>(dmalloc(sampler_sel_bytes(std::max(B, 1))));
     HIPCHK(hipStreamCreateWithFlags(&work, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
@@ -2252,7 +2260,13 @@ int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, fl
     int klo, khi;
     float w;
     h->quantile_ranks(n, klo, khi, w);
-    sampler_step(s, x, eps, B, n, h->coefs, h->step_ctr, noise, 0, 0, 0, klo, khi, w, thresh_out);
+    if (ExtdmHandle::sampler_mw()) {
+      HIPCHK(hipMemsetAsync(h->sel, 0, sampler_sel_bytes(B), s));
+      sampler_step_mw(s, x, eps, B, n, h->coefs, h->step_ctr, noise, 0, 0, 0, klo, khi, w, thresh_out, h->sel,
+                      nullptr, 1);
+    } else {
+      sampler_step(s, x, eps, B, n, h->coefs, h->step_ctr, noise, 0, 0, 0, klo, khi, w, thresh_out);
+    }
     HIPCHK(hipStreamSynchronize(s));  // `c` is a host temporary
   });
 }
@@ -2283,12 +2297,24 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     int klo, khi;
     float w;
     h->quantile_ranks(n, klo, khi, w);
-    auto step = [&]() {
+    const bool mw = ExtdmHandle::sampler_mw();
+    if (mw) {
+      // the selection bins zeroed once; step 0's t set here, every later t (and the step counter)
+      // by the previous step's update launch
+      HIPCHK(hipMemsetAsync(h->sel, 0, sampler_sel_bytes(B), s));
       set_t_from_step(s, h->t_batch, B, h->coefs, h->step_ctr);
+    }
+    auto step = [&]() {
+      if (!mw) set_t_from_step(s, h->t_batch, B, h->coefs, h->step_ctr);
       h->unet_step(B, out, cond_fea, h->eps_buf);
-      sampler_step(s, out, h->eps_buf, B, n, h->coefs, h->step_ctr, noise, seed, sample_base, round, klo, khi, w,
-                   nullptr);
-      incr_counter(s, h->step_ctr);
+      if (mw) {
+        sampler_step_mw(s, out, h->eps_buf, B, n, h->coefs, h->step_ctr, noise, seed, sample_base, round, klo, khi,
+                        w, nullptr, h->sel, h->t_batch, S);
+      } else {
+        sampler_step(s, out, h->eps_buf, B, n, h->coefs, h->step_ctr, noise, seed, sample_base, round, klo, khi, w,
+                     nullptr);
+        incr_counter(s, h->step_ctr);
+      }
     };
     if (use_graph) {
       hipGraph_t graph;

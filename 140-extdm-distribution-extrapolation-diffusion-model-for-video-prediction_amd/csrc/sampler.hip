@@ -130,6 +130,159 @@ __global__ __launch_bounds__(1024) void sampler_step_kernel(float* x, const floa
   }
 }
 
+// ---- multi-workgroup form (round 5): the same step over (chunk, sample) workgroups ----
+// The one-workgroup-per-sample kernel above ran 4 radix passes x up to 2 selections over the whole
+// sample in one workgroup: 4 of 256 CUs busy at UCF's B = 4 (2.6 ms per step) and 64 at BAIR's 64
+// (168 us). Here every pass is a launch over SCH-element chunks x samples: each workgroup counts its
+// chunk's |x0| bytes into LDS bins (filtered by the prefix chosen so far) and adds them into the
+// pass's global bins with integer atomics — exact counts, so the selected order statistics are the
+// same whatever the workgroup order (deterministic, bit-equal to the kernel above). Each workgroup
+// of the next pass re-derives the prefix and residual rank from the earlier passes' bins (a 256-bin
+// scan per selection, one wave each). The final launch derives the two order statistics, the
+// threshold, and updates its chunk; bins live in two sets by step parity, and the final launch
+// zeroes the other set (the previous step's, fully consumed) for the next step. Its last workgroup
+// to finish (a done counter) writes the next step's t and increments the step counter, so the
+// captured step needs no set_t / incr launches.
+constexpr int SCH = 4096;       // elements per workgroup
+constexpr int SNT = 256;        // threads per workgroup
+// selection workspace per sample: [2 sets][4 passes][2 selections][256 bins]
+constexpr int SEL_PER_SAMPLE = 2 * 4 * 2 * 256;
+
+// (prefix, mask, residual rank) of selection `sel` after `npass` passes, from the sample's bins
+// hb = [4 passes][2 sel][256] of the current set (wave-uniform results; called by a whole wave)
+__device__ void derive_sel(const unsigned* hb, int npass, int sel, unsigned rank0, unsigned& prefix, unsigned& mask,
+                           unsigned& rank) {
+  const int l = threadIdx.x & 63;
+  prefix = 0; mask = 0; rank = rank0;
+  for (int p = 0; p < npass; ++p) {
+    const int shift = 24 - 8 * p;
+    const unsigned* h = hb + (p * 2 + sel) * 256;
+    const unsigned h0 = h[4 * l], h1 = h[4 * l + 1], h2 = h[4 * l + 2], h3 = h[4 * l + 3];
+    const unsigned tot = h0 + h1 + h2 + h3;
+    unsigned incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned v = __shfl_up(incl, o);
+      if (l >= o) incl += v;
+    }
+    const unsigned excl = incl - tot;
+    const bool mine = rank >= excl && rank < incl;
+    unsigned d = 4 * l, cum = excl;
+    if (rank >= cum + h0) { cum += h0; ++d;
+      if (rank >= cum + h1) { cum += h1; ++d;
+        if (rank >= cum + h2) { cum += h2; ++d; } } }
+    const unsigned long long bal = __ballot(mine);
+    const int src = bal ? __ffsll((long long)bal) - 1 : 0;
+    d = __shfl(d, src);
+    const unsigned nr = __shfl(rank - cum, src);
+    prefix |= d << shift;
+    mask |= 255u << shift;
+    rank = nr;
+  }
+}
+
+template <int PASS>
+__global__ __launch_bounds__(SNT) void radix_count_kernel(const float* x, const float* eps, int n,
+                                                          const StepCoef* coefs, const int* step_ctr,
+                                                          unsigned* sel, int k_lo, int k_hi) {
+  __shared__ unsigned lh[2][256];
+  __shared__ unsigned st[2][2];  // [sel][prefix, mask]
+  const int b = blockIdx.y;
+  const int step = *step_ctr;
+  const StepCoef c = coefs[step];
+  unsigned* hb = sel + ((size_t)(step & 1) * gridDim.y + b) * (4 * 2 * 256);
+  const int nsel = k_hi == k_lo ? 1 : 2;
+  for (int i = threadIdx.x; i < 512; i += SNT) lh[i >> 8][i & 255] = 0;
+  if (threadIdx.x < 64 * nsel) {
+    const int sl = threadIdx.x >> 6;
+    unsigned pf, mk, rk;
+    derive_sel(hb, PASS, sl, (unsigned)(sl ? k_hi : k_lo), pf, mk, rk);
+    if ((threadIdx.x & 63) == 0) { st[sl][0] = pf; st[sl][1] = mk; }
+  }
+  __syncthreads();
+  const unsigned p0 = st[0][0], m0 = st[0][1];
+  const unsigned p1 = nsel > 1 ? st[1][0] : 0, m1 = nsel > 1 ? st[1][1] : 0;
+  constexpr int shift = 24 - 8 * PASS;
+  const float* xb = x + (long)b * n;
+  const float* eb = eps + (long)b * n;
+  const int e0 = blockIdx.x * SCH, e1 = min(n, e0 + SCH);
+  for (int e = e0 + threadIdx.x; e < e1; e += SNT) {
+    const unsigned u = x0_bits(xb, eb, c, e);
+    if ((u & m0) == p0) atomicAdd(&lh[0][(u >> shift) & 255u], 1u);
+    if (nsel > 1 && (u & m1) == p1) atomicAdd(&lh[1][(u >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256 * nsel; i += SNT) {
+    const unsigned v = lh[i >> 8][i & 255];
+    if (v) atomicAdd(&hb[(PASS * 2 + (i >> 8)) * 256 + (i & 255)], v);
+  }
+}
+
+__global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const float* eps, int n, const StepCoef* coefs,
+                                                            int* step_ctr, const float* noise, int B, uint64_t seed,
+                                                            int sample_base, int round, int k_lo, int k_hi, float q_w,
+                                                            float* thresh_out, unsigned* sel, int* t_next, int nsteps) {
+  __shared__ float vs[2];
+  __shared__ int last;
+  const int b = blockIdx.y;
+  const int step = *step_ctr;
+  const StepCoef c = coefs[step];
+  const int set = step & 1;
+  const unsigned* hb = sel + ((size_t)set * gridDim.y + b) * (4 * 2 * 256);
+  const int nsel = k_hi == k_lo ? 1 : 2;
+  if (threadIdx.x < 64 * nsel) {
+    const int sl = threadIdx.x >> 6;
+    unsigned pf, mk, rk;
+    derive_sel(hb, 4, sl, (unsigned)(sl ? k_hi : k_lo), pf, mk, rk);
+    if ((threadIdx.x & 63) == 0) vs[sl] = __uint_as_float(pf);
+  }
+  // the other set's bins of this sample: the previous step's, consumed; zeroed for the next step
+  // (each of the sample's chunk workgroups takes a share)
+  unsigned* ob = sel + ((size_t)(set ^ 1) * gridDim.y + b) * (4 * 2 * 256);
+  for (int i = blockIdx.x * SNT + threadIdx.x; i < 4 * 2 * 256; i += gridDim.x * SNT) ob[i] = 0;
+  __syncthreads();
+  const float vlo = vs[0], vhi = nsel > 1 ? vs[1] : vs[0];
+  // torch lerp (CPU): w < 0.5 ? a + w (b - a) : b - (b - a)(1 - w)
+  float s = q_w < 0.5f ? vlo + q_w * (vhi - vlo) : vhi - (vhi - vlo) * (1.f - q_w);
+  if (s < 1.f) s = 1.f;
+  if (thresh_out && blockIdx.x == 0 && threadIdx.x == 0) thresh_out[b] = s;
+  float* xb = x + (long)b * n;
+  const float* eb = eps + (long)b * n;
+  const float* nb = noise ? noise + ((long)step * B + b) * n : nullptr;
+  const int e0 = blockIdx.x * SCH, e1 = min(n, e0 + SCH);
+  for (int e = e0 + threadIdx.x; e < e1; e += SNT) {
+    const float xv = xb[e], ev = eb[e];
+    const float x0 = c.sra * xv - c.srm1 * ev;
+    const float xc = fminf(fmaxf(x0, -s), s) / s;
+    float out;
+    if (c.kind == 0) out = c.c1 * xc + c.c2 * xv;
+    else out = xc * c.c1 + c.c2 * ev;
+    if (c.use_noise) {
+      const float z = nb ? nb[e] : philox_normal(seed, sample_base + b, round, step, e);
+      out = out + c.sigma * z;
+    }
+    xb[e] = out;
+  }
+  if (!t_next) return;
+  // the last workgroup to finish advances the step: every workgroup has read *step_ctr above
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* done = reinterpret_cast<int*>(sel + (size_t)2 * gridDim.y * 4 * 2 * 256);
+    last = atomicAdd(done, 1) == (int)(gridDim.x * gridDim.y) - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (step + 1 < nsteps)
+    for (int i = threadIdx.x; i < B; i += SNT) t_next[i] = coefs[step + 1].t;
+  if (threadIdx.x == 0) {
+    int* done = reinterpret_cast<int*>(sel + (size_t)2 * gridDim.y * 4 * 2 * 256);
+    *done = 0;
+    *step_ctr = step + 1;
+  }
+}
+
 __global__ void fill_normal_kernel(float* x, int n, uint64_t seed, int sample_base, int round, int stream_id) {
   const long e = (long)blockIdx.x * 256 + threadIdx.x;
   const int b = blockIdx.y;
@@ -202,6 +355,20 @@ void sampler_step(hipStream_t s, float* x, const float* eps, int B, int n, const
                   int k_hi, float q_w, float* thresh_out) {
   hipLaunchKernelGGL(sampler_step_kernel, dim3(B), dim3(1024), 0, s, x, eps, n, coefs, step_ctr, noise, B, seed,
                      sample_base, round, k_lo, k_hi, q_w, thresh_out);
+}
+
+size_t sampler_sel_bytes(int B) { return ((size_t)B * SEL_PER_SAMPLE + 4) * sizeof(unsigned); }
+
+void sampler_step_mw(hipStream_t s, float* x, const float* eps, int B, int n, const StepCoef* coefs, int* step_ctr,
+                     const float* noise, uint64_t seed, int sample_base, int round, int k_lo, int k_hi, float q_w,
+                     float* thresh_out, unsigned* sel, int* t_next, int nsteps) {
+  const dim3 grid((n + SCH - 1) / SCH, B);
+  hipLaunchKernelGGL(radix_count_kernel<0>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, sel, k_lo, k_hi);
+  hipLaunchKernelGGL(radix_count_kernel<1>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, sel, k_lo, k_hi);
+  hipLaunchKernelGGL(radix_count_kernel<2>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, sel, k_lo, k_hi);
+  hipLaunchKernelGGL(radix_count_kernel<3>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, sel, k_lo, k_hi);
+  hipLaunchKernelGGL(sampler_final_kernel, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, noise, B, seed,
+                     sample_base, round, k_lo, k_hi, q_w, thresh_out, sel, t_next, nsteps);
 }
 
 void fill_normal(hipStream_t s, float* x, int B, int n, uint64_t seed, int sample_base, int round, int stream_id) {
