@@ -338,7 +338,11 @@ struct XPathArgs {
   int T, L, F, LP;
   float* out; long ob, oc, ot; int Cout;
   const _Float16* w; const float* rscale; const float* cbias;
+  // tiles in frame-group-major order (xpath_x3.hip): groups of FG frames, every class's tiles of a
+  // group consecutive; tile_start / tile_last: the class prefix of a full / the last group
+  int FG, ngroups, gtiles, xcd;  // xcd: XCD-contiguous workgroup order (grid a multiple of 8)
   int tile_start[50];
+  int tile_last[50];
 };
 bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
                       const float* cbias);

@@ -21,6 +21,9 @@
 // all output channels; A (the class's packed weights, [kstep][m32][hl][lane][8]) is
 // read straight from L2, B is gathered from the pre-split copy of x (8 consecutive columns per
 // lane and k-step, already hi / lo'). No LDS, no barriers.
+#include <algorithm>
+#include <cstdlib>
+
 #include "kernels.h"
 
 // EXTDM_XP_EXP (diagnostic builds only, results invalid): bit 0 = xpath's output stores predicated off
@@ -96,20 +99,38 @@ __device__ __forceinline__ void class_span(int c, int L, int& start, int& count)
   else { start = L - 7 + c; count = 1; }
 }
 
+// Tile order (round 5): frame groups of FG frames, and within a group every class's tiles
+// consecutively, the groups laid out XCD-contiguously (workgroup j runs on XCD j mod 8 and takes
+// logical slot (j mod 8) nwg / 8 + j / 8). An output line of a border row or column is written by
+// up to four classes (a border column class, the interior, the row class); in the class-major
+// order those writes came hundreds of workgroups apart, after the first partial line had left L2,
+// so each line reached HBM two or three times (PMC WRITE 648 MB for 235 MB of output). Now all
+// classes of a group's frames run back to back on one XCD and the partial writes of a line merge in
+// its L2 before the write-back.
 template <int M32>
 __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lc = lane & 31, h = lane >> 5;
-  const int tile = blockIdx.x * 4 + wave;
-  if (tile >= a.tile_start[49]) return;
-  int cls = 0;  // static indices: a dynamic index into the kernarg array spills it to scratch
+  const int nwg = (int)gridDim.x;
+  const int q = a.xcd ? (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  const int tile = q * 4 + wave;
+  const int total = (a.ngroups - 1) * a.gtiles + a.tile_last[49];
+  if (tile >= total) return;
+  const int g = min(tile / a.gtiles, a.ngroups - 1);
+  const bool lastg = g == a.ngroups - 1;
+  const int lt = tile - g * a.gtiles;
+  int cls = 0, cstart = 0;  // static indices: a dynamic index into the kernarg array spills it to scratch
 #pragma unroll
-  for (int c = 1; c < 49; ++c) cls += tile >= a.tile_start[c];
+  for (int c = 1; c < 49; ++c) {
+    const int st = lastg ? a.tile_last[c] : a.tile_start[c];
+    if (lt >= st) { cls = c; cstart = st; }
+  }
   const int L = a.L;
   int y0, ry, x0, rx;
   class_span(cls / 7, L, y0, ry);
   class_span(cls % 7, L, x0, rx);
-  const int per = ry * rx, npx = a.F * per;
-  const int base = (tile - a.tile_start[cls]) * 64;
+  const int fg = lastg ? a.F - g * a.FG : a.FG;
+  const int per = ry * rx, npx = fg * per;
+  const int base = (lt - cstart) * 64;
 
   int py[2], px[2];
   long xoff[2], ooff[2];
@@ -119,7 +140,7 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
     const int idx = base + nt * 32 + lc;
     ok[nt] = idx < npx;
     const int i = ok[nt] ? idx : 0;
-    const int f = i / per, rem = i - f * per;
+    const int f = g * a.FG + i / per, rem = i - (i / per) * per;
     const int iy = rem / rx, ix = rem - iy * rx;
     const int b = f / a.T, t = f - b * a.T;
     py[nt] = y0 + iy;
@@ -283,13 +304,27 @@ bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void*
   a.T = x.T; a.L = L; a.F = x.B * x.T;
   a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
   a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.cbias = cbias;
-  a.tile_start[0] = 0;
-  for (int c = 0; c < 49; ++c) {
-    const int cy = c / 7, cx = c % 7;
-    const long n = (long)a.F * (cy == 3 ? L - 6 : 1) * (cx == 3 ? L - 6 : 1);
-    a.tile_start[c + 1] = a.tile_start[c] + (int)((n + 63) / 64);
-  }
-  const unsigned blocks = (unsigned)((a.tile_start[49] + 3) / 4);
+  // FG = 8 frames: a group's output (8 x Cout x L^2 x 4 B, 2 MB at BAIR) stays well inside one
+  // XCD's 4 MB L2 while its classes run; the corner classes (one pixel per frame) fill 8 of a
+  // tile's 64 columns. EXTDM_XP_FG overrides (A/B; 0 = the class-major order over all frames).
+  static const int fgv = [] { const char* v = getenv("EXTDM_XP_FG"); return v ? atoi(v) : 32; }();
+  a.FG = fgv > 0 ? std::min(fgv, a.F) : a.F;
+  a.ngroups = (a.F + a.FG - 1) / a.FG;
+  auto prefix = [&](int fg, int* ts) {
+    ts[0] = 0;
+    for (int c = 0; c < 49; ++c) {
+      const int cy = c / 7, cx = c % 7;
+      const long n = (long)fg * (cy == 3 ? L - 6 : 1) * (cx == 3 ? L - 6 : 1);
+      ts[c + 1] = ts[c] + (int)((n + 63) / 64);
+    }
+  };
+  prefix(a.FG, a.tile_start);
+  prefix(a.F - (a.ngroups - 1) * a.FG, a.tile_last);
+  a.gtiles = a.tile_start[49];
+  const long total = (long)(a.ngroups - 1) * a.gtiles + a.tile_last[49];
+  unsigned blocks = (unsigned)((total + 3) / 4);
+  a.xcd = fgv > 0 && blocks >= 64;
+  if (a.xcd) blocks = (blocks + 7) & ~7u;
   if (out.C > 32) hipLaunchKernelGGL(xpath_x3_kernel<2>, dim3(blocks), dim3(256), 0, s, a);
   else hipLaunchKernelGGL(xpath_x3_kernel<1>, dim3(blocks), dim3(256), 0, s, a);
   return true;
