@@ -304,9 +304,11 @@ bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void*
   a.T = x.T; a.L = L; a.F = x.B * x.T;
   a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
   a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.cbias = cbias;
-  // FG = 8 frames: a group's output (8 x Cout x L^2 x 4 B, 2 MB at BAIR) stays well inside one
-  // XCD's 4 MB L2 while its classes run; the corner classes (one pixel per frame) fill 8 of a
-  // tile's 64 columns. EXTDM_XP_FG overrides (A/B; 0 = the class-major order over all frames).
+  // FG = 32 frames (measured sweep at BAIR B = 64, layer 9: 4 / 8 / 16 / 32 / 64 / 112 frames ->
+  // 610 / 515 / 450 / 442 / 432-444 / 502 us, class-major 546 us): smaller groups waste the corner
+  // classes' tiles (one pixel per frame: 32 of a tile's 64 columns at FG = 32) and re-read every
+  // class's weight slice per group; larger ones lose the L2 merge. EXTDM_XP_FG overrides (A/B;
+  // 0 = the class-major order over all frames).
   static const int fgv = [] { const char* v = getenv("EXTDM_XP_FG"); return v ? atoi(v) : 32; }();
   a.FG = fgv > 0 ? std::min(fgv, a.F) : a.F;
   a.ngroups = (a.F + a.FG - 1) / a.FG;
