@@ -3,7 +3,7 @@
 Workload (BASELINE.json configs[1]): BAIR 64x64 ch3, 2 -> 28 (tc = 2, tp = 14
 per autoregressive round x 2 rounds), DDPM 1000 steps, u12 Unet3D (dim 64,
 dim_mults 1,2,4,4) behind the multi_w_ref FlowDiffusion wrapper, random-init
-weights, synthetic clips resident in HBM. BAIR eval default: no occlusion map
+weights, synthetic clips resident in HBM, 128 clips per GPU (WORKLOADS['bair']). BAIR eval default: no occlusion map
 (valid_DM_bair.sh omits --estimate_occlusion_map).
 
 Step accounting. A "step" is one reverse-diffusion step of the per-GPU clip
@@ -117,7 +117,10 @@ def kernel_peak(arith, core_frac=0.0):
 # the BASELINE batch split over its GPU count where it names one (KTH: 64 on 4 GPUs), else
 # what one MI355X runs in a few minutes. The BAIR line is the metric (configs[1]).
 WORKLOADS = {
-    'bair': dict(image=64, tc=2, tp=14, total_pred=28, sampling_steps=1000, timesteps=1000, batch=64, occ=False,
+    # BAIR: 128 clips per GPU (round 5 sweep, DDIM-20 generations on one box: 0.413 / 0.396 / 0.391 /
+    # 0.397 ms per clip-step at B = 64 / 128 / 192 / 256 — the small levels' launches fill the chip
+    # better; 128 keeps one DDPM-1000 generation near 100 s)
+    'bair': dict(image=64, tc=2, tp=14, total_pred=28, sampling_steps=1000, timesteps=1000, batch=128, occ=False,
                  precision=None, baseline='configs[1]: BAIR 64x64 ch3, cond=2 pred=14, DDPM 1000 steps, 1xMI355X'),
     'kth': dict(image=64, tc=10, tp=20, total_pred=40, sampling_steps=100, timesteps=1000, batch=16, occ=False,
                 precision=None, cpu_steady=2, baseline='configs[2]: KTH 64x64 ch1, cond=10 pred=40, DDIM 100 steps, batch=64 on 4 GPUs',
