@@ -14,7 +14,9 @@
 // windows, NT = 1 for windows of <= 32 tokens and for temporal groups (32 / T' pixels'
 // frames, T' = 16 or 32 slots), so no block of the score matrix is wholly masked.
 //   lane = (token column c = lane & 31, half h = lane >> 5); an operand fragment holds the
-//   8 dims 16s + 8h .. +7 of k-step s (dim_head 32: s = 0, 1), so rotary pairs stay in-lane.
+//   8 dims 16s + 8h .. +7 of k-step s (dim_head 32: s = 0, 1; dim_head 16: s = 0 only, the
+//   ada denoiser's C = 256 windows), so rotary pairs stay in-lane. At dim_head 16 the O^T tile's
+//   rows 16-31 (V^T rows past the head) are zero and not stored.
 //   S^T[kt][qt] = K[kt] Q[qt]^T   (NT^2 tiles x 2 k-steps): a lane holds 16 keys of its query
 //   softmax over the keys: in-lane over (kt, r), then the partner half (lane ^ 32)
 //   O^T[qt]    += V^T P^T         P^T straight from the score registers as the B operand
@@ -134,7 +136,7 @@ __device__ __forceinline__ TokB token_b(int tk, const AttnGeom& g, long st, int 
   return o;
 }
 
-template <int MODE, bool X3, int NT>
+template <int MODE, bool X3, int NT, int DH>
 __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict__ qkv, long qsb, long qsc, long st,
                                                         float* __restrict__ o, long osb, long osc, AttnGeom g,
                                                         int heads, int groups_per_sample, int total_groups,
@@ -142,6 +144,8 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
                                                         const float* __restrict__ rcos,
                                                         const float* __restrict__ rsin, float q_scale,
                                                         int* __restrict__ range_flag) {
+  constexpr int KST = DH / 16;  // k-steps of the QK^T contraction
+  constexpr int RH = DH / 2;     // rotary pairs per head
   __shared__ float Vs[4][32 * NT][33];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
   TokB tq[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) tq[t] = token_b<MODE, NT>(32 * t + c, g, st, grp, per);
-  const int hid = heads * 32;
+  const int hid = heads * DH;
   const float* qb = qkv + (long)b * qsb;
   const bool shifted = MODE == 0 && (g.ss0 | g.ss1 | g.ss2) != 0;
   // masks of the 16 keys a lane's score registers hold, per (query tile, key tile): bit r
@@ -178,26 +182,26 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
   int bad = 0;
   for (int hd = wave; hd < heads; hd += 4) {
     // ---- Q, K fragments (token per lane, 16 dims each), rotary in-lane, V to LDS ----
-    Frag<X3> qf[NT][2], kf[NT][2];  // [tile][k-step]
+    Frag<X3> qf[NT][KST], kf[NT][KST];  // [tile][k-step]
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      float qv[16], kv[16];
+      float qv[8 * KST], kv[8 * KST];
       const bool ok = tq[t].valid;
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < KST; ++s)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const int d = 16 * s + 8 * h + e;
-          qv[8 * s + e] = ok ? qb[(long)(hd * 32 + d) * qsc + tq[t].pos] : 0.f;
-          kv[8 * s + e] = ok ? qb[(long)(hid + hd * 32 + d) * qsc + tq[t].pos] : 0.f;
-          Vs[wave][t * 32 + c][d] = ok ? qb[(long)(2 * hid + hd * 32 + d) * qsc + tq[t].pos] : 0.f;
+          qv[8 * s + e] = ok ? qb[(long)(hd * DH + d) * qsc + tq[t].pos] : 0.f;
+          kv[8 * s + e] = ok ? qb[(long)(hid + hd * DH + d) * qsc + tq[t].pos] : 0.f;
+          Vs[wave][t * 32 + c][d] = ok ? qb[(long)(2 * hid + hd * DH + d) * qsc + tq[t].pos] : 0.f;
         }
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < KST; ++s)
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
           const int pi = (16 * s + 8 * h + e) >> 1;
-          const float cs = rcos[tq[t].rpos * 16 + pi], sn = rsin[tq[t].rpos * 16 + pi];
+          const float cs = rcos[tq[t].rpos * RH + pi], sn = rsin[tq[t].rpos * RH + pi];
           const float q0 = qv[8 * s + e] * q_scale, q1 = qv[8 * s + e + 1] * q_scale;
           const float k0 = kv[8 * s + e], k1 = kv[8 * s + e + 1];
           qv[8 * s + e] = q0 * cs - q1 * sn;
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
           kv[8 * s + e + 1] = k1 * cs + k0 * sn;
         }
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < KST; ++s) {
         qf[t][s].set(qv + 8 * s, bad);
         kf[t][s].set(kv + 8 * s, bad);
       }
@@ -225,7 +229,7 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
 #pragma unroll
         for (int r = 0; r < 16; ++r) { sc[kt][r] = 0.f; sx[r] = 0.f; }
 #pragma unroll
-        for (int s = 0; s < 2; ++s) mma(kf[kt][s], qf[qt][s], sc[kt], sx);
+        for (int s = 0; s < KST; ++s) mma(kf[kt][s], qf[qt][s], sc[kt], sx);
         fin<X3>(sc[kt], sx);
       }
       const TokB& me = tq[qt];
@@ -268,7 +272,7 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             pv[e] = sc[kt][8 * s + e] * inv;
-            vv[e] = Vs[wave][kt * 32 + dof(8 * s + e, h)][c];
+            vv[e] = DH == 32 || c < DH ? Vs[wave][kt * 32 + dof(8 * s + e, h)][c] : 0.f;
           }
           Frag<X3> pf, vf;
           pf.template set<false>(pv, bad);
@@ -280,7 +284,8 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
       if (me.valid) {
         float* ob = o + (long)b * osb + me.pos;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) ob[(long)(hd * 32 + dof(r, h)) * osc] = out[r];
+        for (int r = 0; r < 16; ++r)
+          if (DH == 32 || dof(r, h) < DH) ob[(long)(hd * DH + dof(r, h)) * osc] = out[r];
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // Vs reuse by the wave's next head
@@ -294,7 +299,8 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
 bool attention_core(hipStream_t s, const View& qkv, const View& o, const AttnGeom& g, int heads, int dim_head,
                     const float* bias_dense, int bstride, const float* rope_cos, const float* rope_sin, float q_scale,
                     bool bf16) {
-  if (dim_head != 32 || qkv.st != o.st) return false;
+  if ((dim_head != 32 && dim_head != 16) || qkv.st != o.st) return false;
+  if (dim_head == 16 && (g.mode != 0 || bf16)) return false;  // dim 16: the ada C = 256 windows, f16x3
   int groups, nt = 1;
   if (g.mode == 0) {
     const int N = g.ws0 * g.ws1 * g.ws2;
@@ -308,21 +314,25 @@ bool attention_core(hipStream_t s, const View& qkv, const View& o, const AttnGeo
   }
   const int total = qkv.B * groups;
   int* flag = x3_range_ptr();
-#define CORE_GO(M, X, NT_)                                                                                   \
+#define CORE_GO(M, X, NT_, DH_)                                                                              \
   do {                                                                                                       \
-  note_kernel("attn_core_kernel<%d, %s, %d>", M, X ? "true" : "false", NT_);                                  \
-  hipLaunchKernelGGL((attn_core_kernel<M, X, NT_>), dim3(total), dim3(256), 0, s, qkv.p, qkv.sb, qkv.sc, qkv.st,  \
-                     o.p, o.sb, o.sc, g, heads, groups, total, bias_dense, bstride, rope_cos, rope_sin, q_scale, flag); \
+  note_kernel("attn_core_kernel<%d, %s, %d, %d>", M, X ? "true" : "false", NT_, DH_);                         \
+  hipLaunchKernelGGL((attn_core_kernel<M, X, NT_, DH_>), dim3(total), dim3(256), 0, s, qkv.p, qkv.sb, qkv.sc,     \
+                     qkv.st, o.p, o.sb, o.sc, g, heads, groups, total, bias_dense, bstride, rope_cos, rope_sin,    \
+                     q_scale, flag);                                                                          \
   } while (0)
-  if (g.mode == 0 && nt == 2) {
-    if (bf16) CORE_GO(0, false, 2);
-    else CORE_GO(0, true, 2);
+  if (dim_head == 16) {
+    if (nt == 2) CORE_GO(0, true, 2, 16);
+    else CORE_GO(0, true, 1, 16);
+  } else if (g.mode == 0 && nt == 2) {
+    if (bf16) CORE_GO(0, false, 2, 32);
+    else CORE_GO(0, true, 2, 32);
   } else if (g.mode == 0) {
-    if (bf16) CORE_GO(0, false, 1);
-    else CORE_GO(0, true, 1);
+    if (bf16) CORE_GO(0, false, 1, 32);
+    else CORE_GO(0, true, 1, 32);
   } else {
-    if (bf16) CORE_GO(1, false, 1);
-    else CORE_GO(1, true, 1);
+    if (bf16) CORE_GO(1, false, 1, 32);
+    else CORE_GO(1, true, 1, 32);
   }
 #undef CORE_GO
   return true;

@@ -11,6 +11,32 @@ namespace attn_ops {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+// packed fp32 pairs: v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 (two values per VALU issue; hipcc
+// folds splats, swaps and negations into op_sel / op_sel_hi / neg_lo)
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 pair(float a, float b) { f2 v = {a, b}; return v; }
+__device__ __forceinline__ f2 splat(float a) { f2 v = {a, a}; return v; }
+
+// s <- exp2(s c - m) over NT accumulator tiles, returning the lane's sum: the exponent argument and
+// the running sum as packed pairs (16 v_pk_fma + 16 v_pk_add per 32 values instead of 64 VALU)
+template <int NT>
+__device__ __forceinline__ float exp2_sum(f32x16* s, float c, float m) {
+  const f2 c2 = splat(c), m2 = splat(-m);
+  f2 acc = splat(0.f);
+#pragma unroll
+  for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      f2 a = pk_fma(pair(s[kt][r], s[kt][r + 1]), c2, m2);
+      a.x = __builtin_amdgcn_exp2f(a.x);
+      a.y = __builtin_amdgcn_exp2f(a.y);
+      s[kt][r] = a.x;
+      s[kt][r + 1] = a.y;
+      acc += a;
+    }
+  return acc.x + acc.y;
+}
 
 // row of accumulator register r in a 32x32 MFMA tile, lane half h
 __device__ __forceinline__ int dof(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }

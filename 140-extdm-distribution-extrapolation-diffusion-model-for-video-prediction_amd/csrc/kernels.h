@@ -332,12 +332,14 @@ bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& 
 // f16x3 implicit-GEMM conv (conv_gemm_x3.hip): every mode / kernel size of conv_forward's
 // fp32 GEMM; false if the weight has no f16x3 GEMM packing
 // init_conv's x-branch composed with init_noise_conv into 49 border-class 13x13
-// kernels (xpath_x3.hip): out[:, :Cout] = sum_c K_c * x + cbias_c for the 3-channel x
+// kernels (xpath_x3.hip): out[:, :Cout] = sum_c K_c * x + cbias_c (+ add) for the 3-channel x;
+// add (optional, same geometry as out): the hoisted cond_fea branch (runtime fea_hoist_on)
 struct XPathArgs {
   const float* x; long xb, xc, xt;  // the zero-padded pre-split copy (xpad_forward; dwords)
   int T, L, F, LP;
   float* out; long ob, oc, ot; int Cout;
   const _Float16* w; const float* rscale; const float* cbias;
+  const float* add; long ab, ac, at;
   // tiles in frame-group-major order (xpath_x3.hip): groups of FG frames, every class's tiles of a
   // group consecutive; tile_start / tile_last: the class prefix of a full / the last group
   int FG, ngroups, gtiles, xcd;  // xcd: XCD-contiguous workgroup order (grid a multiple of 8)
@@ -345,7 +347,7 @@ struct XPathArgs {
   int tile_last[50];
 };
 bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
-                      const float* cbias);
+                      const float* cbias, const View* add = nullptr);
 // the zero-padded copy of the 3-channel x both kernels above read: [B][3][T][LP][LP], x at
 // (6, 6), LP = xpad_size(L), one dword per position holding its f16x3 pair (hi | lo' << 16,
 // lo' = fp16((v - hi) 2^11)); the range flag (|v| >= 65504) is raised here

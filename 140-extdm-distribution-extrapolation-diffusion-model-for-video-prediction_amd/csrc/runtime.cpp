@@ -676,6 +676,40 @@ struct ExtdmHandle {
     REQUIRE(fea_edges_forward(s, rp, edge, f.C, fw.side, fw.side_scale, fw.corner), "init_conv edge corrections rejected");
   }
 
+  // init_conv's cond_fea branch hoisted out of the reverse step. For ada, ada_u22 and wo_ref the
+  // branch reads only the conditioning map (ada / ada_u22: cond_fea through cond_adaptor +
+  // cond_temporal_attn and the x2 resize, ada.py:1035-1041 / ada_u22.py:1180-1190; wo_ref: cond_fea
+  // itself, wo_ref.py:911-921), which is fixed over a sampling call, and init_conv is linear:
+  // conv(cat(x, f), W) + b = conv(x, W_x) + (conv(f, W_f) + b). prepare_cond evaluates the second
+  // term once over the tp predicted frames (fr_all); each step adds it to the x-branch. u12's
+  // branch reads TrajWarp(x) and stays in the step. EXTDM_NO_FEA_HOIST=1: the per-step conv (A/B).
+  bool fea_hoist_on() const {
+    static const bool off = [] { const char* v = getenv("EXTDM_NO_FEA_HOIST"); return v && v[0] && v[0] != '0'; }();
+    if (off) return false;
+    if (cfg.arch == EXTDM_ARCH_ADA_U22 || cfg.arch == EXTDM_ARCH_WO_REF) return true;
+    return cfg.arch == EXTDM_ARCH_ADA && xpath_enabled();  // ada: added in the x-branch kernel's epilogue
+  }
+  // init_conv.weight split by input channel: "#x" = W[:, :c0] (the x channels), "#f" = W[:, c0:]
+  void split_init_conv(int c0) {
+    if (has("init_conv.weight#x")) return;
+    const HostTensor& w = H("init_conv.weight");
+    const int Co = (int)w.shape[0], Cin = (int)w.shape[1];
+    size_t kk = 1;
+    for (size_t i = 2; i < w.shape.size(); ++i) kk *= (size_t)w.shape[i];
+    REQUIRE(c0 > 0 && c0 < Cin, "init_conv split: bad channel count");
+    for (int part = 0; part < 2; ++part) {
+      const int lo = part ? c0 : 0, hi = part ? Cin : c0;
+      HostTensor t;
+      t.shape = w.shape;
+      t.shape[1] = hi - lo;
+      t.f.resize((size_t)Co * (hi - lo) * kk);
+      for (int m = 0; m < Co; ++m)
+        std::copy(w.f.begin() + ((size_t)m * Cin + lo) * kk, w.f.begin() + ((size_t)m * Cin + hi) * kk,
+                  t.f.begin() + (size_t)m * (hi - lo) * kk);
+      host[part ? "init_conv.weight#f" : "init_conv.weight#x"] = std::move(t);
+    }
+  }
+
   View alloc_cf(int B, int C, int T, int Hh, int Ww) {
     return cf_view(arena.alloc((size_t)B * C * T * Hh * Ww), B, C, T, Hh, Ww);
   }
@@ -1078,9 +1112,10 @@ struct ExtdmHandle {
   }
   // the unfused core path (LN -> qkv 1x1 conv -> attn_core.hip -> proj 1x1 conv + residual): for
   // the shapes the fused f16x3 kernels do not cover (C = 256), in BF16_ATTN always, in F16X3 unless
-  // EXTDM_NO_X3_CORE sends them to the fp32 fused kernels
-  bool core_attn(int ntok, int max_tok, bool fused_x3) const {
-    if (cfg.dim_head != 32 || ntok > max_tok) return false;
+  // EXTDM_NO_X3_CORE sends them to the fp32 fused kernels. dim_head 16 (ada's C = 256 windows):
+  // windows only, f16x3 (attn_core.hip DH = 16)
+  bool core_attn(int ntok, int max_tok, bool fused_x3, bool window) const {
+    if (!(cfg.dim_head == 32 || (cfg.dim_head == 16 && window && !bf16_attn())) || ntok > max_tok) return false;
     if (bf16_attn()) return !fused_x3;
     static const bool off = [] { const char* v = getenv("EXTDM_NO_X3_CORE"); return v && v[0] && v[0] != '0'; }();
     return cfg.precision == EXTDM_PRECISION_F16X3 && !fused_x3 && !off;
@@ -1118,12 +1153,12 @@ struct ExtdmHandle {
               "f16x3 64-token STW launch rejected");
       return;
     }
-    if (core_attn(N, 64, fused_x3)) {
+    if (core_attn(N, 64, fused_x3, true)) {
       // LN + f16x3 qkv conv, the window core (bf16 or f16x3 MFMA), f16x3 proj + residual
       // (bench_stage: extdm_bench_layer times one of the three launches alone)
       last_core = true;
       Scope sc(arena);
-      const int hid = cfg.heads * 32;
+      const int hid = cfg.heads * cfg.dim_head;
       View ln = alloc_cf(x.B, x.C, x.T, x.H, x.W);
       if (!plan && bench_stage == 0) channel_ln(s, ln, x, nullptr, D(p + ".fn.norm.gamma"));
       View qkv = alloc_cf(x.B, 3 * hid, x.T, x.H, x.W);
@@ -1180,7 +1215,7 @@ struct ExtdmHandle {
     AttnGeom g{};
     g.mode = 1; g.D = T; g.H = x.H; g.W = x.W;
     const bool fused_x3 = x3_attn_ok(x.C, T, 1) && out.sc == x.sc && out.st == x.st;
-    if (core_attn(T, 32, fused_x3)) {
+    if (core_attn(T, 32, fused_x3, false)) {
       // double-LN prologue, f16x3 qkv conv, the core (bf16 or f16x3 MFMA), f16x3 to_out + residual
       last_core = true;
       Scope sc(arena);
@@ -1345,6 +1380,7 @@ struct ExtdmHandle {
   // k / v of fm, and for ada / ada_u22 the resized cond_adaptor + cond_temporal_attn
   // features (ada.py:1035-1036), which depend on cond_fea only.
   View r_all, kv_k, kv_v, fup_all, fa_all;  // fa_all: ada's adapted cond_fea at fea_size (phase path)
+  View fr_all;  // the hoisted cond_fea branch of init_conv over the tp predicted frames (fea_hoist_on)
   _Float16* kvp = nullptr;  // k / v as pre-split MFMA fragments (cross_kv_split)
   void alloc_cond_cache() {
     const int Bm = cfg.max_batch, T = frames(), L = cfg.latent, fs = cfg.fea_size;
@@ -1360,6 +1396,8 @@ struct ExtdmHandle {
       fup_all = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * T * L * L * 4), Bm, cfg.fea_ch, T, L, L);
     if (cfg.arch == EXTDM_ARCH_ADA && fea_phase_on())
       fa_all = cf_view(dmalloc((size_t)Bm * cfg.fea_ch * T * fs * fs * 4), Bm, cfg.fea_ch, T, fs, fs);
+    if (fea_hoist_on())
+      fr_all = cf_view(dmalloc((size_t)Bm * cfg.dim * cfg.tp * L * L * 4), Bm, cfg.dim, cfg.tp, L, L);
   }
   static View with_batch(View v, int B) { v.B = B; return v; }
 
@@ -1375,6 +1413,7 @@ struct ExtdmHandle {
       REQUIRE(fs == L, "wo_ref: cond_fea must be at the latent resolution");
       const View fc = vf.frames(0, tc);
       conv(r, vc.frames(0, tc), &fc, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+      hoist_fea(B, vf.frames(tc, cfg.tp));
       return;
     }
     View fup;
@@ -1391,12 +1430,33 @@ struct ExtdmHandle {
       if (!plan) bilinear_frames(s, fu, fa, fa, T);
       fup = fu.frames(0, tc);
     }
+    hoist_fea(B, arch == EXTDM_ARCH_ADA && fa_all.p ? with_batch(fa_all, B).frames(tc, cfg.tp)
+                                                     : with_batch(fup_all, B).frames(tc, cfg.tp));
     if (arch == EXTDM_ARCH_ADA_U22) {  // no init_noise_conv (ada_u22.py:1180)
       conv(r, vc, &fup, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
     } else {
       View x0 = alloc_cf(B, 256, tc, L, L);
       conv(x0, vc, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
       conv(r, x0, &fup, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+    }
+  }
+
+  // fr_all = init_conv's cond_fea branch over the tp predicted frames (fea_hoist_on): f is the
+  // branch's input for those frames (ada with the phase route: the adapted map at fea_size)
+  void hoist_fea(int B, const View& f) {
+    if (!fea_hoist_on()) return;
+    const View fr = with_batch(fr_all, B);
+    if (cfg.arch == EXTDM_ARCH_ADA) {  // the biases ride in the x-branch kernel's class bias
+      if (fa_all.p) {
+        if (!plan) HIPCHK(hipMemsetAsync(fr.p, 0, (size_t)fr.numel() * sizeof(float), s));
+        fea_phase_conv(fr, f);
+      } else {
+        Pxpath();
+        conv(fr, f, nullptr, P("init_conv.weight#fea"), 1, 3, nullptr);
+      }
+    } else {
+      split_init_conv(3);
+      conv(fr, f, nullptr, P("init_conv.weight#f"), 1, 3, D("init_conv.bias"));
     }
   }
 
@@ -1426,7 +1486,12 @@ struct ExtdmHandle {
     {
       Scope sc(arena);
       View rp = r.frames(tc, tp);
-      if (arch == EXTDM_ARCH_WO_REF) {
+      const bool hoist = fea_hoist_on();
+      const View fr = hoist ? with_batch(fr_all, B) : View{};
+      if (hoist && (arch == EXTDM_ARCH_WO_REF || arch == EXTDM_ARCH_ADA_U22)) {
+        split_init_conv(3);
+        conv(rp, vx, nullptr, P("init_conv.weight#x"), 1, 3, nullptr, &fr);  // + cond_fea branch + bias
+      } else if (arch == EXTDM_ARCH_WO_REF) {
         const View fp = vf.frames(tc, tp);
         conv(rp, vx, &fp, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
       } else if (arch == EXTDM_ARCH_ADA_U22) {
@@ -1470,7 +1535,11 @@ struct ExtdmHandle {
           fu = with_batch(fup_all, B).frames(tc, tp);
           if (fa_all.p) fpre = with_batch(fa_all, B).frames(tc, tp);
         }
-        if (xp) {
+        if (xp && hoist) {
+          // ada: rp = K_class * x + cbias_class + the hoisted cond_fea branch, one launch
+          const XPathW& xw = Pxpath();
+          if (!plan) REQUIRE(xpath_x3_forward(s, rp, xpad, xw.w, xw.rs, xw.cb, &fr), "composed init_conv launch rejected");
+        } else if (xp) {
           // rp = K_class * x + cbias_class (x-branch + both biases), then rp += Wb * pad(up2(F))
           const XPathW& xw = Pxpath();
           if (!plan) REQUIRE(xpath_x3_forward(s, rp, xpad, xw.w, xw.rs, xw.cb), "composed init_conv launch rejected");
@@ -2501,6 +2570,8 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     // layers 0 / 11 with the phase-composed cond_fea branch (fea_x3.hip): 0 = the 5x5 phase conv
     // over F (fea_size, 4 x dim rows, += into r as the forward issues it), 11 = its edge
     // corrections (the two line launches and the corner launch)
+    REQUIRE(!((layer == 0 || layer == 11) && h->fea_hoist_on()),
+            "bench layers 0 / 11: init_conv's cond_fea branch is hoisted out of the step (cond cache)");
     if ((layer == 0 || layer == 11) && h->fea_phase_on()) {
       const int fs = h->cfg.fea_size, Cf = h->cfg.fea_ch, Co = h->cfg.dim;
       View f = h->alloc_cf(B, Cf, T, fs, fs), r = h->alloc_cf(B, Co, T, L, L);

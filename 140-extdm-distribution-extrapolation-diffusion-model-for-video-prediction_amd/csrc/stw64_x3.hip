@@ -212,12 +212,17 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
 #pragma unroll
       for (int e = 0; e < 8; ++e) { const float d = xv[k][e] - m1; v += d * d; }
     v = xh_sum(v);
-    // padded tokens normalise to 0 through a 0 factor (stw_x3.hip: no select per element)
+    // padded tokens normalise to 0 through a 0 factor (stw_x3.hip: no select per element); packed
+    // pairs, the same operation order as the scalar ((x - m) rv) gamma
     const float rv = (1.f / sqrtf(v / C + 1e-5f)) * (valid ? 1.f : 0.f);
 #pragma unroll
     for (int k = 0; k < KS; ++k)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) xv[k][e] = (xv[k][e] - m1) * rv * ldb(rs_g, 32 * h, (16 * k + e) * 4);
+      for (int e = 0; e < 8; e += 2) {
+        const f2 t = (pair(xv[k][e], xv[k][e + 1]) - splat(m1)) * splat(rv) *
+                     pair(ldb(rs_g, 32 * h, (16 * k + e) * 4), ldb(rs_g, 32 * h, (16 * k + e + 1) * 4));
+        xv[k][e] = t.x; xv[k][e + 1] = t.y;
+      }
     // the wave's largest |value| to [2^8, 2^9) (stw_x3.hip: e_w; exact power-of-two scaling,
     // folded back through the q / k / v factors, so the two waves of a window may differ)
     float am = 0.f;
@@ -235,7 +240,10 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) xv[k][e] *= gs;
+      for (int e = 0; e < 8; e += 2) {
+        const f2 t = pair(xv[k][e], xv[k][e + 1]) * splat(gs);
+        xv[k][e] = t.x; xv[k][e + 1] = t.y;
+      }
       split8(xv[k], xh[k], xl[k], bad);
     }
   }
@@ -317,7 +325,8 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
         const _Float16* fv = W + UL::V + s * UL::FRAG + lane * 8;
         v = mma3(xh[s], xl[s], *reinterpret_cast<const h8*>(fv), *reinterpret_cast<const h8*>(fv + 512), v);
       }
-      // scale, RoPE on (d, d + 1) = registers (r, r + 1)
+      // scale, RoPE on (d, d + 1) = registers (r, r + 1), as packed pairs:
+      // (x0, x1) <- (x0, x1) c + (-x1, x0) s
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         float q0 = q[r], q1 = q[r + 1], k0 = k[r], k1 = k[r + 1];
@@ -332,7 +341,12 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
       for (int s = 0; s < 2; ++s) {
         float tq[8], tk_[8], tv[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { tq[e] = q[8 * s + e]; tk_[e] = k[8 * s + e]; tv[e] = v[8 * s + e] * sv; }
+        for (int e = 0; e < 8; e += 2) {
+          tq[e] = q[8 * s + e]; tq[e + 1] = q[8 * s + e + 1];
+          tk_[e] = k[8 * s + e]; tk_[e + 1] = k[8 * s + e + 1];
+          const f2 t = pair(v[8 * s + e], v[8 * s + e + 1]) * splat(sv);  // both tiles' V at one scale
+          tv[e] = t.x; tv[e + 1] = t.y;
+        }
         Op<BF> kf, vf;
         qf[s].set(tq, bad);
         kf.set(tk_, bad);
@@ -377,17 +391,8 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
       mx = xh_max(mx);
       // P' = 16 exp(s - mx) = v_exp_f32 of fma(s, log2 e 2^-(e_q+e_k), 4 - mx ...) (masked -inf -> 0),
       // unnormalised: O is scaled by 16 / sum P' after PV (16 or 8 products instead of 32)
-      const float mxl = mx * csm - 4.f;
-      float sum = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          sc_[kt][r] = __builtin_amdgcn_exp2f(fmaf(sc_[kt][r], csm, -mxl));
-          sum += sc_[kt][r];
-        }
-      sum = xh_sum(sum);
-      const float inv = 16.f / sum;  // O carries P = 16 p (stw_x3.hip operand-scale note)
+      const float sum = xh_sum(exp2_sum<2>(sc_, csm, mx * csm - 4.f));
+      const float inv = 16.f * __builtin_amdgcn_rcpf(sum);  // O carries P = 16 p
       // O^T[dd][i] += sum_j V^T[dd][j] P'^T[j][i]
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
@@ -403,8 +408,11 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
         }
       // the head's rows: all 16 registers (dim 32), registers 8 hh .. 8 hh + 7 (dim 16)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (HPU == 1 || (r >> 3) == hh) o[hh][r] *= inv;
+      for (int r = 0; r < 16; r += 2)
+        if (HPU == 1 || (r >> 3) == hh) {
+          const f2 t = pair(o[hh][r], o[hh][r + 1]) * splat(inv);
+          o[hh][r] = t.x; o[hh][r + 1] = t.y;
+        }
     }
     // projection: Y[c][i] += sum_dd Wp[c][u*32 + dd] O^T[dd][i] (f16x3)
 #pragma unroll
@@ -443,9 +451,12 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int cu = ct * 32 + (r & 3) + 8 * (r >> 2);
-        tileL[(cu + 4 * h) * TCS + tpos] = pacc[ct][r] * spj + ldb(rs_b, 16 * h, cu * 4);
+      for (int r = 0; r < 16; r += 2) {
+        const int cu = ct * 32 + (r & 3) + 8 * (r >> 2);  // r + 1: row cu + 1
+        const f2 y = pair(pacc[ct][r], pacc[ct][r + 1]) * splat(spj) +
+                     pair(ldb(rs_b, 16 * h, cu * 4), ldb(rs_b, 16 * h, (cu + 1) * 4));
+        tileL[(cu + 4 * h) * TCS + tpos] = y.x;
+        tileL[(cu + 1 + 4 * h) * TCS + tpos] = y.y;
       }
     __syncthreads();
     u32x2 xr[PPW];
@@ -459,10 +470,8 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const u32x2 y = *reinterpret_cast<const u32x2*>(tileL + pc.lbase + i * CPI * TCS);
-      u32x2 o;
-      o[0] = __float_as_uint(__uint_as_float(y[0]) + __uint_as_float(xr[i][0]));
-      o[1] = __float_as_uint(__uint_as_float(y[1]) + __uint_as_float(xr[i][1]));
-      __builtin_amdgcn_raw_buffer_store_b64(o, rs_x, goff_of(pc, i), 0, 0);
+      const f2 sum2 = __builtin_bit_cast(f2, y) + __builtin_bit_cast(f2, xr[i]);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, sum2), rs_x, goff_of(pc, i), 0, 0);
     }
   } else if (dbg & 8) {  // timing only: no epilogue loads / stores (one store keeps the work live)
     float acc = 0.f;

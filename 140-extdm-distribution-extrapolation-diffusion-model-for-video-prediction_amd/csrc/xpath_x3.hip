@@ -133,7 +133,7 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
   const int base = (lt - cstart) * 64;
 
   int py[2], px[2];
-  long xoff[2], ooff[2];
+  long xoff[2], ooff[2], aoff[2];
   bool ok[2];
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
@@ -147,6 +147,7 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
     px[nt] = x0 + ix;
     xoff[nt] = (long)b * a.xb + (long)t * a.xt + (long)py[nt] * a.LP + px[nt];  // padded: row py + dy, col px + 8h
     ooff[nt] = (long)b * a.ob + (long)t * a.ot + (long)py[nt] * L + px[nt];
+    aoff[nt] = (long)b * a.ab + (long)t * a.at + (long)py[nt] * L + px[nt];
   }
 
   f32x16 acc[M32][2];
@@ -195,7 +196,11 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
 #if EXTDM_XP_EXP & 1
         if (acc[m][nt][r] == 12345.678f)
 #endif
-        if (row < a.Cout) a.out[ooff[nt] + (long)row * a.oc] = acc[m][nt][r] * rs[row] + cb[row];
+        if (row < a.Cout) {
+          float v = acc[m][nt][r] * rs[row] + cb[row];
+          if (a.add) v += a.add[aoff[nt] + (long)row * a.ac];
+          a.out[ooff[nt] + (long)row * a.oc] = v;
+        }
       }
   }
 }
@@ -294,16 +299,18 @@ bool noise_pool_x3_forward(hipStream_t s, const View& out, const View& x, const 
 
 // x: the zero-padded copy (xpad_forward; LP = x.W, the latent L = out.H)
 bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
-                      const float* cbias) {
+                      const float* cbias, const View* add) {
   const int L = out.H;
   if (x.C != 3 || x.W != x.H || x.W != xpad_size(L) || x.st != (long)x.W * x.H || out.W != L || L < 7 ||
       out.C > 64 || out.T != x.T || out.B != x.B)
     return false;
+  if (add && (add->B != out.B || add->C != out.C || add->T != out.T || add->H != L || add->W != L)) return false;
   XPathArgs a{};
   a.x = x.p; a.xb = x.sb; a.xc = x.sc; a.xt = x.st; a.LP = x.W;
   a.T = x.T; a.L = L; a.F = x.B * x.T;
   a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
   a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.cbias = cbias;
+  if (add) { a.add = add->p; a.ab = add->sb; a.ac = add->sc; a.at = add->st; }
   // FG = 32 frames (measured sweep at BAIR B = 64, layer 9: 4 / 8 / 16 / 32 / 64 / 112 frames ->
   // 610 / 515 / 450 / 442 / 432-444 / 502 us, class-major 546 us): smaller groups waste the corner
   // classes' tiles (one pixel per frame: 32 of a tile's 64 columns at FG = 32) and re-read every

@@ -85,16 +85,16 @@ def kernel_arith(kname, precision):
     """The arithmetic of a launched kernel, from its template: 'fp32' (fp32 MFMA), 'f16x3' (three
     fp16 MFMAs per fp32 product), 'bf16', or 'f16x3+bf16' (the fused attention kernels in
     BF16_ATTN: qkv / proj on f16x3, QK^T / PV on bf16).
-      attn_core_kernel<MODE, X3, NT>         X3 true: f16x3, false: bf16
-      attn_x3_kernel<C, MODE, DH, NW, TILE, BF>, stw64_x3_kernel<C, DH, NW, BF>
+      attn_core_kernel<MODE, X3, NT, DH>     X3 true: f16x3, false: bf16
+      attn_x3_kernel<C, MODE, DH, NW, TILE, BF>, stw64_x3_kernel<C, DH, NW, BF, TILE>
                                              BF false: f16x3, true: f16x3+bf16
     Other families by name (FP32_FAMILIES / X3_FAMILIES); unknown names by the handle's precision."""
     ident, args = _template(kname)
-    if ident == 'attn_core_kernel' and len(args) == 3:
+    if ident == 'attn_core_kernel' and len(args) in (3, 4):
         return 'f16x3' if args[1] == 'true' else 'bf16'
     if ident == 'attn_x3_kernel' and len(args) == 6:
         return 'f16x3+bf16' if args[5] == 'true' else 'f16x3'
-    if ident == 'stw64_x3_kernel' and len(args) == 4:
+    if ident == 'stw64_x3_kernel' and len(args) in (4, 5):
         return 'f16x3+bf16' if args[3] == 'true' else 'f16x3'
     if ident in FP32_FAMILIES:
         return 'fp32'

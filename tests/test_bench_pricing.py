@@ -38,3 +38,38 @@ def test_mixed_bf16_attention_peak(kname):
     p = bench.kernel_peak('f16x3+bf16', f)
     assert F16X3 < p < 2516.6
     assert 1 / p == pytest.approx((1 - f) / F16X3 + f / 2516.6)
+
+
+@pytest.mark.parametrize('kname,arith', [
+    ('stw64_x3_kernel<64, 32, 8, true, true>', 'f16x3+bf16'),
+    ('stw64_x3_kernel<128, 16, 4, false, false>', 'f16x3'),
+    ('attn_core_kernel<0, true, 2, 16>', 'f16x3'),
+    ('attn_core_kernel<0, false, 1, 32>', 'bf16'),
+])
+def test_current_template_arity(kname, arith):
+    """The names the library reports today (five stw64 / four attn_core template arguments)."""
+    assert bench.kernel_arith(kname, 'fp32') == arith
+
+
+def test_note_kernel_formats_are_parsed_by_template():
+    """Every note_kernel format string in csrc/ for the families kernel_arith reads by argument
+    (attn_core, attn_x3, stw64) parses by its template, not the by-name fallback: a format with a
+    new argument count must fail here rather than price a bf16 kernel as f16x3."""
+    import glob
+    import os
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = glob.glob(os.path.join(root, '*_amd', 'csrc', '*.hip'))
+    assert csrc
+    seen = set()
+    for path in csrc:
+        for m in re.finditer(r'note_kernel\("((\w+)<[^"]*>)"', open(path).read()):
+            fmt, ident = m.group(1), m.group(2)
+            if ident not in ('attn_core_kernel', 'attn_x3_kernel', 'stw64_x3_kernel'):
+                continue
+            seen.add(ident)
+            name = fmt.replace('%d', '64').replace('%s', 'true')
+            # by template: the bf16 flag set -> never the precision fallback ('fp32' here)
+            assert bench.kernel_arith(name, 'fp32') in ('bf16', 'f16x3+bf16', 'f16x3'), fmt
+            assert bench.kernel_arith(name, 'fp32') != 'f16x3' or ident == 'attn_core_kernel', fmt
+    assert seen == {'attn_core_kernel', 'attn_x3_kernel', 'stw64_x3_kernel'}

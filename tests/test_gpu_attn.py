@@ -148,6 +148,19 @@ def test_window64_attention_vs_oracle(name, prefix, level, shifted):
     parity_log.check(err, ATT_BAR)
 
 
+# ada's C = 256 levels (dim_head 16, 64-token windows): the unfused route with the f16x3 attention
+# core at DH = 16 (attn_core.hip), LN -> qkv 1x1 conv -> core -> proj 1x1 conv + residual
+W64_CORE = [('ada_kth', 'downs.2.1', 2, True), ('ada_kth', 'downs.2.3', 2, False)]
+
+
+@pytest.mark.parametrize('name,prefix,level,shifted', W64_CORE)
+def test_window64_dim16_core_vs_oracle(name, prefix, level, shifted):
+    x, out, ref = _w64_case(name, prefix, level, shifted, 'f16x3')
+    err = (out - ref).abs().max().item()
+    print(f'{name} {prefix} f16x3 core max|err| {err:.3e}')
+    parity_log.check(err, ATT_BAR)
+
+
 @pytest.mark.parametrize('name,prefix,level,shifted', W64)
 def test_window64_attention_bf16_vs_oracle(name, prefix, level, shifted):
     """bf16 attention contractions (BF16_ATTN): q, k, v and P rounded to bf16 (2^-9 relative

@@ -445,8 +445,10 @@ def test_fea_phase_fs32_vs_oracle(arch):
     eps = gpu_eps(h, x, t, cond, fea)
     # the route: at fs 32 the two-phase 128 x 256 tile's X window (12 rows x 36 = 432 staging
     # slots > 400) is not covered, so fea_phase_on (runtime.cpp) keeps the bilinear + 7x7 route
-    # — decided once per handle by a dry run of both launchers, no hard failure (round-4 ADVICE)
-    with pytest.raises(RuntimeError, match='phase-composed cond_fea branch is off'):
+    # — decided once per handle by a dry run of both launchers, no hard failure (round-4 ADVICE);
+    # ada's branch reads only cond_fea and runs once per call in the cond cache (fea_hoist_on)
+    msg = 'phase-composed cond_fea branch is off' if arch == 'u12' else 'hoisted out of the step'
+    with pytest.raises(RuntimeError, match=msg):
         h.bench_layer(1, 11, 1)
     with torch.no_grad():
         ref = oracle().unet_forward(make_sd(cfg), cfg.as_dict(), x, t, cond, fea)
