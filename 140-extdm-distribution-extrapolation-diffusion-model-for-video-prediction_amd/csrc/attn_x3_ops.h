@@ -11,13 +11,6 @@ namespace attn_ops {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
-// packed fp32 pairs: v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 (two values per VALU issue; hipcc
-// folds splats, swaps and negations into op_sel / op_sel_hi / neg_lo)
-typedef float f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f2 pair(float a, float b) { f2 v = {a, b}; return v; }
-__device__ __forceinline__ f2 splat(float a) { f2 v = {a, a}; return v; }
-
 // s <- exp2(s c - m) over NT accumulator tiles, returning the lane's sum: the exponent argument and
 // the running sum as packed pairs (16 v_pk_fma + 16 v_pk_add per 32 values instead of 64 VALU)
 template <int NT>

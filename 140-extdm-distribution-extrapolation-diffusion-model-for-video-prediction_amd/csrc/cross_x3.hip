@@ -345,9 +345,10 @@ __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __rest
       }
       float cm = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sh[r] = fmaf(sx[r], LO_DN, sh[r]);
-        cm = fmaxf(cm, sh[r]);
+      for (int r = 0; r < 16; r += 2) {  // packed pairs (v_pk_fma_f32)
+        const f2 t = pk_fma(pair(sx[r], sx[r + 1]), splat(LO_DN), pair(sh[r], sh[r + 1]));
+        sh[r] = t.x; sh[r + 1] = t.y;
+        cm = fmaxf(cm, fmaxf(t.x, t.y));
       }
       const int j0 = 32 * kt;
       if (j0 + 32 > NK) {  // partial tail tile (wave-uniform)
@@ -368,13 +369,17 @@ __global__ __launch_bounds__(256) void cross_attn_x3p_kernel(const float* __rest
         for (int r = 0; r < 16; ++r) { oh[u][r] *= alpha; ox[u][r] *= alpha; ox2[u][r] *= alpha; }
         mk[u] = mn;
       }
-      float ps = 0.f;
       const float mkb = mk[u] - 11.f;  // P' = 2^11 P
+      f2 ps2 = splat(0.f);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sh[r] = __builtin_amdgcn_exp2f(sh[r] - mkb);
-        ps += sh[r];
+      for (int r = 0; r < 16; r += 2) {  // packed argument and sum (v_pk_add_f32)
+        f2 a = pair(sh[r], sh[r + 1]) - splat(mkb);
+        a.x = __builtin_amdgcn_exp2f(a.x);
+        a.y = __builtin_amdgcn_exp2f(a.y);
+        sh[r] = a.x; sh[r + 1] = a.y;
+        ps2 += a;
       }
+      const float ps = ps2.x + ps2.y;
       l[u] += ps + __shfl_xor(ps, 32);
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {

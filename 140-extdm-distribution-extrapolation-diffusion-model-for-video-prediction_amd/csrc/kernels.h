@@ -72,6 +72,12 @@ __device__ __forceinline__ H8 lo_dn(const H8& w) {
 // hi is rounded once and lo reads that rounded register, so the two cannot disagree.
 typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
+// packed fp32 pairs: v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 (two values per VALU issue; hipcc
+// folds splats, swaps and negations into op_sel / op_sel_hi / neg_lo)
+typedef f32x2_t f2;
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 pair(float a, float b) { f2 v = {a, b}; return v; }
+__device__ __forceinline__ f2 splat(float a) { f2 v = {a, a}; return v; }
 __device__ __forceinline__ void split2c(float a, float b, f16x2_t& hi, f16x2_t& lo) {
   hi = __builtin_convertvector((f32x2_t){a, b}, f16x2_t);
   // an opaque 1.0: with a literal, instcombine turns the fma into fsub of a converted hi

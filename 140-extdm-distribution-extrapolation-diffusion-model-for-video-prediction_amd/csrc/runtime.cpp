@@ -2484,7 +2484,9 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
           REQUIRE(noise_pool_x3_forward(s, q, xp, nw.w, nw.rs, h->D("init_noise_conv.bias")), "bench layer 10: launch rejected");
         };
       }
+      note_kernel("");
       launch();
+      h->bench_kernel[layer] = noted_kernel();
       hipEvent_t e0, e1;
       HIPCHK(hipEventCreate(&e0));
       HIPCHK(hipEventCreate(&e1));

@@ -538,12 +538,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     for (int s = 0; s < 2; ++s) {
       float tq[8], tk[8], tv[8];
 #pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        tq[e] = q[8 * s + e]; tq[e + 1] = q[8 * s + e + 1];
-        tk[e] = k[8 * s + e]; tk[e + 1] = k[8 * s + e + 1];
-        const f2 t = pair(v[8 * s + e], v[8 * s + e + 1]) * splat(sv);
-        tv[e] = t.x; tv[e + 1] = t.y;
-      }
+      for (int e = 0; e < 8; ++e) { tq[e] = q[8 * s + e]; tk[e] = k[8 * s + e]; tv[e] = v[8 * s + e] * sv; }
       qf[s].set(tq, bad);
       kf[s].set(tk, bad);
       vf[s].set(tv, bad);
@@ -563,22 +558,23 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       for (int s = 0; s < 2; ++s)
         if (HPU == 1 || s == hh) sc_ = mmo(kf[s], qf[s], sc_);
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const f2 t = pair(sc_[r], sc_[r + 1]) + pair(bia[hh][r], bia[hh][r + 1]);
-        sc_[r] = t.x; sc_[r + 1] = t.y;
-      }
+      for (int r = 0; r < 16; ++r) sc_[r] += bia[hh][r];
       float mx = -INFINITY;
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc_[r]);
       mx = xh_max(mx);
       // exp(s - mx) as v_exp_f32 (2^x) of fma(s, log2 e, -mx log2 e): masked -inf -> 0
-      const float sum = xh_sum(exp2_sum<1>(&sc_, csm, mx * csm));
-      const float inv = 16.f * __builtin_amdgcn_rcpf(sum);  // P * 2^4 (wsc header note)
+      const float mxl = mx * csm;
+      float sum = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const f2 t = pair(sc_[r], sc_[r + 1]) * splat(inv);
-        sc_[r] = t.x; sc_[r + 1] = t.y;
+      for (int r = 0; r < 16; ++r) {
+        sc_[r] = __builtin_amdgcn_exp2f(fmaf(sc_[r], csm, -mxl));
+        sum += sc_[r];
       }
+      sum = xh_sum(sum);
+      const float inv = 16.f / sum;  // P * 2^4 (wsc header note)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc_[r] *= inv;
       // O^T[dd][i] = sum_j V^T[dd][j] P^T[j][i]; lanes of the unit's other head masked
       const bool mine = HPU == 1 || (lc / DH) == hh;
 #pragma unroll

@@ -17,7 +17,7 @@
 //
 // The kernel is an implicit GEMM per class: M = Cout (32 * M32), K = 3 ch x 13 rows x
 // 16 columns (13 used), N = the class's pixels over all frames (a class's pixel set
-// is rows(cy) x cols(cx) of every frame). One wave owns 64 pixels (two n32 tiles) and
+// is rows(cy) x cols(cx) of every frame). One wave owns 32 NT pixels (NT n32 tiles) and
 // all output channels; A (the class's packed weights, [kstep][m32][hl][lane][8]) is
 // read straight from L2, B is gathered from the pre-split copy of x (8 consecutive columns per
 // lane and k-step, already hi / lo'). No LDS, no barriers.
@@ -107,8 +107,10 @@ __device__ __forceinline__ void class_span(int c, int L, int& start, int& count)
 // so each line reached HBM two or three times (PMC WRITE 648 MB for 235 MB of output). Now all
 // classes of a group's frames run back to back on one XCD and the partial writes of a line merge in
 // its L2 before the write-back.
-template <int M32>
-__global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
+// NT: n32 tiles (32-pixel columns) per wave sharing each A fragment load: 2 (64 px) or 4 (128 px:
+// half the per-pixel weight reads from L2, twice the accumulators)
+template <int M32, int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void xpath_x3_kernel(XPathArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lc = lane & 31, h = lane >> 5;
   const int nwg = (int)gridDim.x;
   const int q = a.xcd ? (int)(blockIdx.x & 7) * (nwg >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
@@ -130,13 +132,13 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
   class_span(cls % 7, L, x0, rx);
   const int fg = lastg ? a.F - g * a.FG : a.FG;
   const int per = ry * rx, npx = fg * per;
-  const int base = (lt - cstart) * 64;
+  const int base = (lt - cstart) * (32 * NT);
 
-  int py[2], px[2];
-  long xoff[2], ooff[2], aoff[2];
-  bool ok[2];
+  int py[NT], px[NT];
+  long xoff[NT], ooff[NT], aoff[NT];
+  bool ok[NT];
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
+  for (int nt = 0; nt < NT; ++nt) {
     const int idx = base + nt * 32 + lc;
     ok[nt] = idx < npx;
     const int i = ok[nt] ? idx : 0;
@@ -150,11 +152,11 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
     aoff[nt] = (long)b * a.ab + (long)t * a.at + (long)py[nt] * L + px[nt];
   }
 
-  f32x16 acc[M32][2];
+  f32x16 acc[M32][NT];
 #pragma unroll
   for (int m = 0; m < M32; ++m)
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
+    for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[m][nt][r] = 0.f;
 
@@ -173,11 +175,11 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
         ah[m] = *reinterpret_cast<const h8*>(ap);
         al[m] = *reinterpret_cast<const h8*>(ap + 512);
       }
-      h8 bh[2], bl[2];
+      h8 bh[NT], bl[NT];
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) gather8p(xc + xoff[nt] + dy * a.LP, bh[nt], bl[nt]);
+      for (int nt = 0; nt < NT; ++nt) gather8p(xc + xoff[nt] + dy * a.LP, bh[nt], bl[nt]);
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
+      for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int m = 0; m < M32; ++m) acc[m][nt] = mma3(ah[m], al[m], bh[nt], bl[nt], acc[m][nt]);
     }
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(256) void xpath_x3_kernel(XPathArgs a) {
   const float* rs = a.rscale + (long)cls * M32 * 32;
   const float* cb = a.cbias + (long)cls * M32 * 32;
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
+  for (int nt = 0; nt < NT; ++nt) {
     if (!ok[nt]) continue;
 #pragma unroll
     for (int m = 0; m < M32; ++m)
@@ -319,12 +321,15 @@ bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void*
   static const int fgv = [] { const char* v = getenv("EXTDM_XP_FG"); return v ? atoi(v) : 32; }();
   a.FG = fgv > 0 ? std::min(fgv, a.F) : a.F;
   a.ngroups = (a.F + a.FG - 1) / a.FG;
+  // EXTDM_XP_NT: pixels per wave = 32 NT (2: 64 px, 4: 128 px)
+  static const int ntv = [] { const char* v = getenv("EXTDM_XP_NT"); return v && atoi(v) == 4 ? 4 : 2; }();
+  const int TPX = 32 * ntv;
   auto prefix = [&](int fg, int* ts) {
     ts[0] = 0;
     for (int c = 0; c < 49; ++c) {
       const int cy = c / 7, cx = c % 7;
       const long n = (long)fg * (cy == 3 ? L - 6 : 1) * (cx == 3 ? L - 6 : 1);
-      ts[c + 1] = ts[c] + (int)((n + 63) / 64);
+      ts[c + 1] = ts[c] + (int)((n + TPX - 1) / TPX);
     }
   };
   prefix(a.FG, a.tile_start);
@@ -334,8 +339,15 @@ bool xpath_x3_forward(hipStream_t s, const View& out, const View& x, const void*
   unsigned blocks = (unsigned)((total + 3) / 4);
   a.xcd = fgv > 0 && blocks >= 64;
   if (a.xcd) blocks = (blocks + 7) & ~7u;
-  if (out.C > 32) hipLaunchKernelGGL(xpath_x3_kernel<2>, dim3(blocks), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(xpath_x3_kernel<1>, dim3(blocks), dim3(256), 0, s, a);
+  if (ntv == 4) {
+    note_kernel("xpath_x3_kernel<%d, 4>", out.C > 32 ? 2 : 1);
+    if (out.C > 32) hipLaunchKernelGGL((xpath_x3_kernel<2, 4>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((xpath_x3_kernel<1, 4>), dim3(blocks), dim3(256), 0, s, a);
+  } else {
+    note_kernel("xpath_x3_kernel<%d, 2>", out.C > 32 ? 2 : 1);
+    if (out.C > 32) hipLaunchKernelGGL((xpath_x3_kernel<2, 2>), dim3(blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((xpath_x3_kernel<1, 2>), dim3(blocks), dim3(256), 0, s, a);
+  }
   return true;
 }
 

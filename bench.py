@@ -311,7 +311,7 @@ class NativeWorkload:
               (8, 'mfma', 'cross_attn_x3p_kernel<1>', 'TrajWarp cross-attention core (3584 queries x 512 keys, 8 heads)'),
               (4, 'hbm', None,
                'level-0 res_conv 128->64 1x1x1'),
-              (9, 'mfma', 'xpath_x3_kernel<2>', 'init_conv x-branch as one composed 13x13 conv 3->64, K = 3x169'),
+              (9, 'mfma', 'xpath_x3_kernel', 'init_conv x-branch as one composed 13x13 conv 3->64, K = 3x169'),
               (10, 'mfma', 'noise_pool_x3_kernel', 'init_noise_conv 3->256 1x7x7 + MaxPool(1,2,2), K = 3x49'),
               (12, 'hbm', 'pw_x3_kernel',
                'TrajWarp linear_q 256->256 1x1 + ReLU, weights register-resident (pw_x3)'),

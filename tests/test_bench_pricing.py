@@ -19,7 +19,7 @@ F16X3 = 2516.6 / 3
     ('window_attn_kernel', 'f16x3', 'fp32', 157.3),
     ('conv_x3_kernel<3, 1, 64, 256, 1, 4, 4, 2, true, 2, false, false, 0, false, false>', 'fp32', 'f16x3', F16X3),
     ('cross_attn_x3p_kernel<1>', 'f16x3', 'f16x3', F16X3),
-    ('xpath_x3_kernel<2>', 'f16x3', 'f16x3', F16X3),
+    ('xpath_x3_kernel<2, 2>', 'f16x3', 'f16x3', F16X3),
     ('conv_kernel<3, 64>', 'f16x3', 'fp32', 157.3),
 ])
 def test_peak_by_template(kname, precision, arith, peak):
