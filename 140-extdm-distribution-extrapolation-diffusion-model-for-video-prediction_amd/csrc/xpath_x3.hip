@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void x
 // lane half h takes row 2*dyp + h of the pair. Pool: rows within the lane (nt), columns
 // with the partner lane (lane ^ 1, same rows of the accumulator).
 constexpr int NP_MW = 2;
-__global__ __launch_bounds__(256) void noise_pool_x3_kernel(NoisePoolArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void noise_pool_x3_kernel(NoisePoolArgs a) {
   // m32 tiles per wave: 2 (64 rows), so accumulators + operands fit two waves per SIMD
   // (MW = 4 took 158 VGPRs + 128 AGPRs: one wave per SIMD, every k-step's L2 loads exposed)
   constexpr int MW = NP_MW;
