@@ -211,25 +211,30 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   // a half-wave (8 rows x 4 columns of one channel) read 32 distinct banks ((a/4) mod 32 for
   // 4-B accesses; shifted windows straddle two chunks at complementary column offsets).
   static_assert(!TILE || (C == 64 && NW == 8), "tile path: C = 64, 8 waves");
-  // T0: the MODE 0 tile above. T1: MODE 1 (temporal, 16 frames, two pixels per wave): the
-  // workgroup's 16 consecutive pixels x 16 frames x C, as [c][16-B chunk q][frame t][4 px]
-  // (one 1-KiB LDS-DMA instruction per channel: lane l = (q = l >> 4, t = l & 15) loads the
-  // 16 B of pixels 4q .. 4q+3 of frame t), so the prologue reads x from LDS (2-way bank
-  // conflicts: frames t and t + 8 share banks), the residual comes from the tile and the
-  // output leaves as 16-B row pieces; gamma and the inner LayerNorm's w / b are in LDS too.
+  // T0: the MODE 0 tile above. T1: MODE 1 (temporal attention over PER = 16 frame slots, two
+  // pixels per wave, or PER = 32, one pixel per wave; D <= PER frames): the workgroup's
+  // 32 NW / PER consecutive pixels x PER frames x C, as [c][16-B chunk q][frame t][4 px] (one
+  // 1-KiB LDS-DMA instruction per channel: lane l = (q = l / PER, t = l % PER) loads the 16 B of
+  // pixels 4q .. 4q+3 of frame t; slots t >= D re-read frame D - 1 and are masked, never stored),
+  // so the prologue reads x from LDS (2-way bank conflicts: frames t and t + 8 share banks), the
+  // residual comes from the tile and the output leaves as 16-B row pieces; gamma and the inner
+  // LayerNorm's w / b are in LDS too. (Round 5: PER = 32 and D < PER, for KTH's 30, SMMNIST's 20
+  // and Cityscapes' 7 frames, whose per-lane loads touched one cache line per frame and channel.)
   // The per-lane path spent 31.7K of ~112K cycles per wave in the prologue (strided x loads and
   // per-element parameter loads) and 23.4K in the epilogue (s_memtime stamps, B = 64).
   constexpr bool T0 = TILE && MODE == 0, T1 = TILE && MODE == 1;
   float* const tileT = reinterpret_cast<float*>(wsm + 2 * UL::HALVES);
   // behind the tile: T0 gamma + proj bias, T1 gamma + LayerNorm w + b (192 floats)
   float* const parL = tileT + C * 256;
-  const int hw0 = T1 ? ((wg * NW) % groups_per_sample) * 2 : 0;  // T1: the workgroup's first pixel
+  const int PER = g.D <= 16 ? 16 : 32;                                     // T1: frame slots per pixel
+  const int hw0 = T1 ? ((wg * NW) % groups_per_sample) * (32 / PER) : 0;  // T1: the workgroup's first pixel
   if (T1) {
+    const int lt = lane % PER, lq = lane / PER;
+    const long loff = (long)(lt < g.D ? lt : g.D - 1) * st + hw0 + 4 * lq;
 #pragma unroll
     for (int i = 0; i < C / NW; ++i) {
       const int c = wave + i * NW;
-      __builtin_amdgcn_global_load_lds((const void*)(xb + (long)c * sc + (lane & 15) * st + hw0 + 4 * (lane >> 4)),
-                                       (lds_ptr_t)(tileT + c * 256), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(xb + (long)c * sc + loff), (lds_ptr_t)(tileT + c * 256), 16, 0, 0);
     }
     if (wave == 0 && lane < 48)
       __builtin_amdgcn_global_load_lds((const void*)(lane < 16 ? gamma + 4 * lane
@@ -238,8 +243,9 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  // T1: this lane's (frame, pixel) in the tile
-  const int t1idx = ((2 * wave + (lc >> 4)) >> 2) * 64 + (lc & 15) * 4 + ((2 * wave + (lc >> 4)) & 3);
+  // T1: this lane's (frame, pixel) in the tile: pixel pw of the workgroup, frame slot lc % PER
+  const int t1pw = (32 / PER) * wave + lc / PER;
+  const int t1idx = (t1pw >> 2) * (4 * PER) + (lc % PER) * 4 + (t1pw & 3);
   int trow[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // element offset of tile row r in a channel plane
   if (T0) {
     const int grp0 = (wg * NW) % groups_per_sample;
@@ -726,12 +732,13 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
       }
     __syncthreads();
     float* o0 = ob + hw0;
+    const int lt = lane % PER, lq = lane / PER;  // id & 63 == lane below (NW * 64 is a multiple of 64)
 #pragma unroll
     for (int i = 0; i < C * 64 / (NW * 64); ++i) {
       const int id = tid + i * NW * 64;
-      const int c = id >> 6, l = id & 63;
-      const float4 v = *reinterpret_cast<const float4*>(tileT + c * 256 + 4 * l);
-      *reinterpret_cast<float4*>(o0 + (long)c * osc + (long)(l & 15) * st + 4 * (l >> 4)) = v;
+      const int c = id >> 6;
+      const float4 v = *reinterpret_cast<const float4*>(tileT + c * 256 + 4 * lane);
+      if (lt < g.D) *reinterpret_cast<float4*>(o0 + (long)c * osc + (long)lt * st + 4 * lq) = v;
     }
     stamp(19);
   } else if (MODE == 1 && lds_epi) {
@@ -820,11 +827,15 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   }
 }
 
-// The MODE 1 tile path (kernel, T1): 16 frames, whole workgroups of 16 pixels inside a sample,
-// 16-B aligned rows; x and out share their channel / frame strides (temporal_x3).
+// The MODE 1 tile path (kernel, T1): D <= 32 frames (16 or 32 slots per pixel), whole workgroups
+// of 16 / 8 pixels inside a sample, 16-B aligned rows; x and out share their channel / frame
+// strides (temporal_x3). EXTDM_X3_TILE1_16=1: only D = 16, the round-4 scope (A/B).
 bool attn_x3_tile1_ok(const View& x, const View& out, const AttnGeom& g, int groups) {
   static const bool off = [] { const char* v = getenv("EXTDM_X3_NO_TILE"); return v && v[0] && v[0] != '0'; }();
-  return !off && g.mode == 1 && g.D == 16 && (g.H * g.W) % 16 == 0 && groups % 8 == 0 && x.st == (long)x.H * x.W &&
+  static const bool only16 = [] { const char* v = getenv("EXTDM_X3_TILE1_16"); return v && v[0] && v[0] != '0'; }();
+  const int per = g.D <= 16 ? 16 : 32;
+  return !off && g.mode == 1 && g.D >= 1 && g.D <= 32 && (!only16 || g.D == 16) && (g.H * g.W) % (256 / per) == 0 &&
+         groups % 8 == 0 && x.st == (long)x.H * x.W &&
          x.st % 4 == 0 && x.sc % 4 == 0 && x.sb % 4 == 0 && out.sc % 4 == 0 && out.sb % 4 == 0 && out.st == x.st &&
          ((uintptr_t)x.p & 15) == 0 && ((uintptr_t)out.p & 15) == 0;
 }

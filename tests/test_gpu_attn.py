@@ -171,3 +171,32 @@ def test_window64_attention_bf16_vs_oracle(name, prefix, level, shifted):
     print(f'{name} {prefix} bf16_attn max|err| {err:.3e} = {err / inc:.2e} x max|increment|')
     parity_log.check(err, 1e-2 * inc, f'bf16, max|increment| {inc:.3e}')
     assert err > 1e-7  # a different arithmetic from the fp32-faithful mode
+
+
+# temporal attention at the other configs' frame counts: KTH 30 (dim_head 16), wo_ref 14 (the golden
+# config's tc - 1 + tp), Cityscapes 7 — the LDS tile path with 32 / 16 frame slots per pixel and the slots
+# past D masked (stw_x3.hip T1, round 5)
+TEMPORAL = [('ada_kth', 'init_temporal_attn'), ('woref_smmnist', 'init_temporal_attn'),
+            ('u22_city', 'init_temporal_attn')]
+
+
+@pytest.mark.parametrize('name,prefix', TEMPORAL)
+def test_temporal_frame_counts_vs_oracle(name, prefix):
+    from oracle import extdm_oracle as O
+    cfg = CONFIGS[name]
+    h, sd = handle(name, 'f16x3')
+    C, L = cfg.dim, cfg.latent
+    gen = torch.Generator().manual_seed(41)
+    x = torch.randn(2, C, cfg.frames, L, L, generator=gen) * 1.5 + 0.3
+    out = torch.empty(x.shape, device=DEV)
+    h.attn_layer(prefix, x.to(DEV), out, shifted=False)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        ref = O.temporal_attention(sd, prefix, x, O.time_pos_bias(sd, cfg.frames), cfg.heads, cfg.dim_head)
+    err = (out.cpu() - ref).abs().max().item()
+    out2 = torch.empty(x.shape, device=DEV)
+    h.attn_layer(prefix, x.to(DEV), out2, shifted=False)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), out2.cpu())
+    print(f'{name} {prefix} D={cfg.frames} max|err| {err:.3e}')
+    parity_log.check(err, ATT_BAR, f'D = {cfg.frames}')
