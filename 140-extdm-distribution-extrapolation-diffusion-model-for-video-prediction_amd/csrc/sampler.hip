@@ -46,6 +46,25 @@ __device__ __forceinline__ float philox_normal(uint64_t seed, int sample, int ro
   return (lane & 1) ? rad * sn : rad * cs;
 }
 
+// the four normals of one Philox block (e0 % 4 == 0): exactly philox_normal(e0 + i), i = 0..3 —
+// one Philox call and two Box-Muller pairs instead of four calls and four pairs
+__device__ __forceinline__ void philox_normal4(uint64_t seed, int sample, int round, int step, long e0, float z[4]) {
+  const uint4 ctr = make_uint4((unsigned)(e0 >> 2), (unsigned)step, (unsigned)round, 0x5EEDu);
+  const uint2 key = make_uint2((unsigned)seed ^ (unsigned)sample * 0x85EBCA6Bu, (unsigned)(seed >> 32) + (unsigned)sample);
+  const uint4 r = philox4x32_10(ctr, key);
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const unsigned a = p ? r.z : r.x, b2 = p ? r.w : r.y;
+    const float u1 = ((float)a + 1.0f) * 2.3283064365386963e-10f;  // (0, 1]
+    const float u2 = (float)b2 * 2.3283064365386963e-10f;
+    const float rad = sqrtf(-2.0f * logf(u1));
+    float sn, cs;
+    sincosf(6.283185307179586f * u2, &sn, &cs);
+    z[2 * p] = rad * cs;
+    z[2 * p + 1] = rad * sn;
+  }
+}
+
 // |x0| bit pattern of element e (recomputed from x and eps on every pass: the
 // sample's 2 x 4n bytes stay L2-resident, so nothing is held in registers).
 __device__ __forceinline__ unsigned x0_bits(const float* xb, const float* eb, const StepCoef& c, int e) {
@@ -250,18 +269,41 @@ __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const floa
   const float* eb = eps + (long)b * n;
   const float* nb = noise ? noise + ((long)step * B + b) * n : nullptr;
   const int e0 = blockIdx.x * SCH, e1 = min(n, e0 + SCH);
-  for (int e = e0 + threadIdx.x; e < e1; e += SNT) {
-    const float xv = xb[e], ev = eb[e];
+  auto update = [&](float xv, float ev, float z) __attribute__((always_inline)) {
     const float x0 = c.sra * xv - c.srm1 * ev;
     const float xc = fminf(fmaxf(x0, -s), s) / s;
     float out;
     if (c.kind == 0) out = c.c1 * xc + c.c2 * xv;
     else out = xc * c.c1 + c.c2 * ev;
-    if (c.use_noise) {
-      const float z = nb ? nb[e] : philox_normal(seed, sample_base + b, round, step, e);
-      out = out + c.sigma * z;
+    if (c.use_noise) out = out + c.sigma * z;
+    return out;
+  };
+  if ((n & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(eps) & 15) == 0 &&
+      (!nb || (reinterpret_cast<uintptr_t>(noise) & 15) == 0)) {
+    // four consecutive elements per thread (16-B loads and stores; one Philox block per four)
+    for (int e = e0 + 4 * threadIdx.x; e < e1; e += 4 * SNT) {
+      const float4 x4 = *reinterpret_cast<const float4*>(xb + e), e4 = *reinterpret_cast<const float4*>(eb + e);
+      float z[4] = {0.f, 0.f, 0.f, 0.f};
+      if (c.use_noise) {
+        if (nb) {
+          const float4 n4 = *reinterpret_cast<const float4*>(nb + e);
+          z[0] = n4.x; z[1] = n4.y; z[2] = n4.z; z[3] = n4.w;
+        } else {
+          philox_normal4(seed, sample_base + b, round, step, e, z);
+        }
+      }
+      float4 o;
+      o.x = update(x4.x, e4.x, z[0]);
+      o.y = update(x4.y, e4.y, z[1]);
+      o.z = update(x4.z, e4.z, z[2]);
+      o.w = update(x4.w, e4.w, z[3]);
+      *reinterpret_cast<float4*>(xb + e) = o;
     }
-    xb[e] = out;
+  } else {
+    for (int e = e0 + threadIdx.x; e < e1; e += SNT) {
+      const float z = c.use_noise ? (nb ? nb[e] : philox_normal(seed, sample_base + b, round, step, e)) : 0.f;
+      xb[e] = update(xb[e], eb[e], z);
+    }
   }
   if (!t_next) return;
   // the last workgroup to finish advances the step: every workgroup has read *step_ctr above
