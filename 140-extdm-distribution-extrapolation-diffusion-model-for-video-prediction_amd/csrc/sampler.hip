@@ -306,8 +306,12 @@ __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const floa
     }
   }
   if (!t_next) return;
-  // the last workgroup to finish advances the step: every workgroup has read *step_ctr above
-  __threadfence();
+  // the last workgroup to finish advances the step: every workgroup has read *step_ctr above (its
+  // value fed this workgroup's coefficient loads before its count below). No device-scope fence:
+  // nothing written here is read inside this launch (x, the zeroed bin set, t_next and the counter
+  // are read by the next launches, after the kernel boundary), and on gfx950 a release fence writes
+  // back the XCD's whole L2 — issued by each of the B x n / 4096 workgroups it cost ~150 us per
+  // BAIR step at 128 clips.
   __syncthreads();
   if (threadIdx.x == 0) {
     int* done = reinterpret_cast<int*>(sel + (size_t)2 * gridDim.y * 4 * 2 * 256);
@@ -315,7 +319,6 @@ __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const floa
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();
   if (step + 1 < nsteps)
     for (int i = threadIdx.x; i < B; i += SNT) t_next[i] = coefs[step + 1].t;
   if (threadIdx.x == 0) {
