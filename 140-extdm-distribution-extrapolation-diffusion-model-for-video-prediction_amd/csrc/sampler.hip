@@ -159,9 +159,9 @@ __global__ __launch_bounds__(1024) void sampler_step_kernel(float* x, const floa
 // of the next pass re-derives the prefix and residual rank from the earlier passes' bins (a 256-bin
 // scan per selection, one wave each). The final launch derives the two order statistics, the
 // threshold, and updates its chunk; bins live in two sets by step parity, and the final launch
-// zeroes the other set (the previous step's, fully consumed) for the next step. One one-workgroup
-// launch then writes the next step's t and increments the step counter (sampler_advance_kernel,
-// replacing the set_t / incr pair).
+// zeroes the other set (the previous step's, fully consumed) for the next step. Its last workgroup
+// to finish (a done counter) writes the next step's t and increments the step counter, so the
+// captured step needs no set_t / incr launches.
 constexpr int SCH = 4096;       // elements per workgroup
 constexpr int SNT = 256;        // threads per workgroup
 // selection workspace per sample: [2 sets][4 passes][2 selections][256 bins]
@@ -242,6 +242,7 @@ __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const floa
                                                             int sample_base, int round, int k_lo, int k_hi, float q_w,
                                                             float* thresh_out, unsigned* sel, int* t_next, int nsteps) {
   __shared__ float vs[2];
+  __shared__ int last;
   const int b = blockIdx.y;
   const int step = *step_ctr;
   const StepCoef c = coefs[step];
@@ -304,20 +305,24 @@ __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const floa
       xb[e] = update(xb[e], eb[e], z);
     }
   }
-}
-
-// t and the step counter for the next step (one workgroup, after the update launch). Folding this
-// into the update launch (its last workgroup, found by a global completion count) needed a
-// device-scope release fence in every workgroup before the count — on gfx950 a write-back of the
-// XCD's whole L2, issued by each of the B x n / 4096 workgroups: ~150 us per BAIR step at 128 clips;
-// without the fences the next step's kernels saw stale counters across XCDs (two-rank bench test).
-__global__ __launch_bounds__(256) void sampler_advance_kernel(int* step_ctr, const StepCoef* coefs, int* t_next, int B,
-                                                              int nsteps) {
-  const int step = *step_ctr;
+  if (!t_next) return;
+  // the last workgroup to finish advances the step: every workgroup has read *step_ctr above
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* done = reinterpret_cast<int*>(sel + (size_t)2 * gridDim.y * 4 * 2 * 256);
+    last = atomicAdd(done, 1) == (int)(gridDim.x * gridDim.y) - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
   if (step + 1 < nsteps)
-    for (int i = threadIdx.x; i < B; i += 256) t_next[i] = coefs[step + 1].t;
-  __syncthreads();  // every thread has read the counter
-  if (threadIdx.x == 0) *step_ctr = step + 1;
+    for (int i = threadIdx.x; i < B; i += SNT) t_next[i] = coefs[step + 1].t;
+  if (threadIdx.x == 0) {
+    int* done = reinterpret_cast<int*>(sel + (size_t)2 * gridDim.y * 4 * 2 * 256);
+    *done = 0;
+    *step_ctr = step + 1;
+  }
 }
 
 __global__ void fill_normal_kernel(float* x, int n, uint64_t seed, int sample_base, int round, int stream_id) {
@@ -406,7 +411,6 @@ void sampler_step_mw(hipStream_t s, float* x, const float* eps, int B, int n, co
   hipLaunchKernelGGL(radix_count_kernel<3>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, sel, k_lo, k_hi);
   hipLaunchKernelGGL(sampler_final_kernel, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, noise, B, seed,
                      sample_base, round, k_lo, k_hi, q_w, thresh_out, sel, t_next, nsteps);
-  if (t_next) hipLaunchKernelGGL(sampler_advance_kernel, dim3(1), dim3(256), 0, s, step_ctr, coefs, t_next, B, nsteps);
 }
 
 void fill_normal(hipStream_t s, float* x, int B, int n, uint64_t seed, int sample_base, int round, int stream_id) {
