@@ -159,9 +159,9 @@ __global__ __launch_bounds__(1024) void sampler_step_kernel(float* x, const floa
 // of the next pass re-derives the prefix and residual rank from the earlier passes' bins (a 256-bin
 // scan per selection, one wave each). The final launch derives the two order statistics, the
 // threshold, and updates its chunk; bins live in two sets by step parity, and the final launch
-// zeroes the other set (the previous step's, fully consumed) for the next step. Its last workgroup
-// to finish (a done counter) writes the next step's t and increments the step counter, so the
-// captured step needs no set_t / incr launches.
+// zeroes the other set (the previous step's, fully consumed) for the next step. One one-workgroup
+// launch then writes the next step's t and increments the step counter (sampler_advance_kernel,
+// replacing the set_t / incr pair).
 constexpr int SCH = 4096;       // elements per workgroup
 constexpr int SNT = 256;        // threads per workgroup
 // selection workspace per sample: [2 sets][4 passes][2 selections][256 bins]
@@ -176,7 +176,13 @@ __device__ void derive_sel(const unsigned* hb, int npass, int sel, unsigned rank
   for (int p = 0; p < npass; ++p) {
     const int shift = 24 - 8 * p;
     const unsigned* h = hb + (p * 2 + sel) * 256;
-    const unsigned h0 = h[4 * l], h1 = h[4 * l + 1], h2 = h[4 * l + 2], h3 = h[4 * l + 3];
+    // device-scope atomic loads: the bins were built by other launches' device-scope atomics, and a
+    // plain load may hit a stale copy of the line in this XCD's L2 (kernel boundaries do not
+    // invalidate it; DESIGN.md §5 sampler note)
+    const unsigned h0 = __hip_atomic_load(h + 4 * l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned h1 = __hip_atomic_load(h + 4 * l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned h2 = __hip_atomic_load(h + 4 * l + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned h3 = __hip_atomic_load(h + 4 * l + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned tot = h0 + h1 + h2 + h3;
     unsigned incl = tot;
 #pragma unroll
@@ -242,7 +248,6 @@ __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const floa
                                                             int sample_base, int round, int k_lo, int k_hi, float q_w,
                                                             float* thresh_out, unsigned* sel, int* t_next, int nsteps) {
   __shared__ float vs[2];
-  __shared__ int last;
   const int b = blockIdx.y;
   const int step = *step_ctr;
   const StepCoef c = coefs[step];
@@ -258,7 +263,8 @@ __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const floa
   // the other set's bins of this sample: the previous step's, consumed; zeroed for the next step
   // (each of the sample's chunk workgroups takes a share)
   unsigned* ob = sel + ((size_t)(set ^ 1) * gridDim.y + b) * (4 * 2 * 256);
-  for (int i = blockIdx.x * SNT + threadIdx.x; i < 4 * 2 * 256; i += gridDim.x * SNT) ob[i] = 0;
+  for (int i = blockIdx.x * SNT + threadIdx.x; i < 4 * 2 * 256; i += gridDim.x * SNT)
+    __hip_atomic_store(ob + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // at the atomics' coherence point
   __syncthreads();
   const float vlo = vs[0], vhi = nsel > 1 ? vs[1] : vs[0];
   // torch lerp (CPU): w < 0.5 ? a + w (b - a) : b - (b - a)(1 - w)
@@ -305,24 +311,20 @@ __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const floa
       xb[e] = update(xb[e], eb[e], z);
     }
   }
-  if (!t_next) return;
-  // the last workgroup to finish advances the step: every workgroup has read *step_ctr above
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int* done = reinterpret_cast<int*>(sel + (size_t)2 * gridDim.y * 4 * 2 * 256);
-    last = atomicAdd(done, 1) == (int)(gridDim.x * gridDim.y) - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
+}
+
+// t and the step counter for the next step (one workgroup, after the update launch). Folding this
+// into the update launch (its last workgroup, found by a global completion count) needed a
+// device-scope release fence in every workgroup before the count — on gfx950 a write-back of the
+// XCD's whole L2, issued by each of the B x n / 4096 workgroups: ~150 us per BAIR step at 128 clips;
+// without the fences the next step's kernels saw stale counters across XCDs (two-rank bench test).
+__global__ __launch_bounds__(256) void sampler_advance_kernel(int* step_ctr, const StepCoef* coefs, int* t_next, int B,
+                                                              int nsteps) {
+  const int step = *step_ctr;
   if (step + 1 < nsteps)
-    for (int i = threadIdx.x; i < B; i += SNT) t_next[i] = coefs[step + 1].t;
-  if (threadIdx.x == 0) {
-    int* done = reinterpret_cast<int*>(sel + (size_t)2 * gridDim.y * 4 * 2 * 256);
-    *done = 0;
-    *step_ctr = step + 1;
-  }
+    for (int i = threadIdx.x; i < B; i += 256) t_next[i] = coefs[step + 1].t;
+  __syncthreads();  // every thread has read the counter
+  if (threadIdx.x == 0) *step_ctr = step + 1;
 }
 
 __global__ void fill_normal_kernel(float* x, int n, uint64_t seed, int sample_base, int round, int stream_id) {
@@ -411,6 +413,7 @@ void sampler_step_mw(hipStream_t s, float* x, const float* eps, int B, int n, co
   hipLaunchKernelGGL(radix_count_kernel<3>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, sel, k_lo, k_hi);
   hipLaunchKernelGGL(sampler_final_kernel, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, noise, B, seed,
                      sample_base, round, k_lo, k_hi, q_w, thresh_out, sel, t_next, nsteps);
+  if (t_next) hipLaunchKernelGGL(sampler_advance_kernel, dim3(1), dim3(256), 0, s, step_ctr, coefs, t_next, B, nsteps);
 }
 
 void fill_normal(hipStream_t s, float* x, int B, int n, uint64_t seed, int sample_base, int round, int stream_id) {
