@@ -9,7 +9,7 @@ LIB_PATH = os.environ.get('EXTDM_LIB') or os.path.join(HERE, 'libextdm_hip.so')
 
 # every symbol include/extdm.h declares
 EXPORTS = ['extdm_create', 'extdm_destroy', 'extdm_last_error', 'extdm_load_weight', 'extdm_finalize',
-           'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_bench_layer', 'extdm_bench_layer_kernel',
+           'extdm_workspace_bytes', 'extdm_unet_forward', 'extdm_sample', 'extdm_sampler_step', 'extdm_record_thresholds', 'extdm_bench_layer', 'extdm_bench_layer_kernel',
            'extdm_decode', 'extdm_set_lfae', 'extdm_region_params', 'extdm_region_hw', 'extdm_bg_params',
            'extdm_flow_predict', 'extdm_flow_hw', 'extdm_bottleneck', 'extdm_range_flag',
            'extdm_attn_layer', 'extdm_frame_metrics_workspace', 'extdm_frame_metrics', 'extdm_bilinear_frames']
@@ -75,6 +75,8 @@ def load():
     L.extdm_sample.restype = i32
     L.extdm_sampler_step.argtypes = [vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp]
     L.extdm_sampler_step.restype = i32
+    L.extdm_record_thresholds.argtypes = [vp, vp, i64]
+    L.extdm_record_thresholds.restype = i32
     L.extdm_bench_layer.argtypes = [vp, i32, i32, i32, ctypes.POINTER(f32), ctypes.POINTER(ctypes.c_double)]
     L.extdm_bench_layer.restype = i32
     L.extdm_bench_layer_kernel.argtypes = [vp, i32, ctypes.c_char_p, i32]
@@ -248,6 +250,13 @@ class Handle:
         _require_device(x, eps, noise, thresh_out)
         check(load().extdm_sampler_step(self.h, x.shape[0], sampler, int(t), int(t_next), float(eta), _ptr(x),
                                         _ptr(eps), _ptr(noise), _ptr(thresh_out), _stream()))
+
+    def record_thresholds(self, buf):
+        """Record every later sample() call's per-step thresholds into buf[k * B + b] (device
+        fp32; None stops). The tensor must stay alive while recording is on."""
+        _require_device(buf)
+        self._thresh_buf = buf
+        check(load().extdm_record_thresholds(self.h, _ptr(buf), 0 if buf is None else buf.numel()))
 
     def range_flag(self, reset=True):
         """1 if an f16x3 conv input reached |v| >= 65504 since the last reset."""

@@ -402,15 +402,16 @@ struct StepCoef {  // per sampler step (host-computed in fp32 exactly like the r
 void sampler_step(hipStream_t s, float* x, const float* eps, int B, int n, const StepCoef* coefs,
                   const int* step_ctr, const float* noise /*[S][B][n] or null*/, uint64_t seed, int sample_base,
                   int round, int k_lo, int k_hi, float q_w, float* thresh_out);
-// The same step over (4096-element chunk, sample) workgroups (sampler.hip, round 5): four radix
-// count launches and the update launch. sel: the selection workspace (sampler_sel_bytes(B)), zeroed
-// before the first step of a call (B = the launched batch: its layout depends on it). t_next
-// non-null: the update's last workgroup writes coefs[step + 1].t to t_next[0 .. B) (if step + 1 <
-// nsteps) and increments *step_ctr (the captured step's set_t / incr).
-size_t sampler_sel_bytes(int B);
+// The same step over (4096-element chunk, sample) workgroups (sampler.hip): four radix count
+// launches, the update launch and (t_next non-null) a one-workgroup launch that writes
+// coefs[step + 1].t to t_next[0 .. B) (if step + 1 < nsteps) and increments *step_ctr (the captured
+// step's set_t / incr). ws: the selection workspace, sampler_sel_bytes(B, n) bytes for the launched
+// B and n (its layout depends on both); it needs no initialisation. thresh_out (both forms, may be
+// null): the threshold of sample b at step k goes to thresh_out[k * B + b].
+size_t sampler_sel_bytes(int B, int n);
 void sampler_step_mw(hipStream_t s, float* x, const float* eps, int B, int n, const StepCoef* coefs, int* step_ctr,
                      const float* noise, uint64_t seed, int sample_base, int round, int k_lo, int k_hi, float q_w,
-                     float* thresh_out, unsigned* sel, int* t_next, int nsteps);
+                     float* thresh_out, unsigned* ws, int* t_next, int nsteps);
 void fill_normal(hipStream_t s, float* x, int B, int n, uint64_t seed, int sample_base, int round, int stream_id);
 void set_t_from_step(hipStream_t s, int* t_batch, int B, const StepCoef* coefs, const int* step_ctr);
 void incr_counter(hipStream_t s, int* ctr);

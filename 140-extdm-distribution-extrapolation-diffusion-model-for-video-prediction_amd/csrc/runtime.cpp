@@ -117,7 +117,9 @@ struct ExtdmHandle {
   const bool fuse_res_gn = [] { const char* v = getenv("EXTDM_NO_RES_GN"); return !(v && v[0] && v[0] != '0'); }();
   int* t_batch = nullptr;
   int* step_ctr = nullptr;
-  unsigned* sel = nullptr;  // the multi-workgroup sampler step's selection bins (sampler_sel_bytes)
+  unsigned* sel = nullptr;  // the multi-workgroup sampler step's selection workspace (sampler_sel_bytes)
+  float* thresh_rec = nullptr;  // extdm_record_thresholds: per-step thresholds of extdm_sample, [S][B]
+  int64_t thresh_cap = 0;
   // the sampler step over (chunk, sample) workgroups (sampler.hip); EXTDM_SAMPLER_1WG=1 restores the
   // one-workgroup-per-sample kernel with its set_t / incr launches (A/B)
   static bool sampler_mw() {
@@ -2126,7 +2128,7 @@ struct ExtdmHandle {
     partials = reinterpret_cast<double*>(dmalloc(((size_t)B * 8 * 64 * 2 + (size_t)B * 8 + (size_t)B * 512) * sizeof(double)));
     t_batch = reinterpret_cast<int*>(dmalloc((size_t)std::max(B, 1) * sizeof(int)));
     step_ctr = reinterpret_cast<int*>(dmalloc(sizeof(int) * 4));
-    sel = reinterpret_cast<unsigned*>(dmalloc(sampler_sel_bytes(std::max(B, 1))));
+    sel = reinterpret_cast<unsigned*>(dmalloc(sampler_sel_bytes(std::max(B, 1), (int)n)));
     HIPCHK(hipStreamCreateWithFlags(&work, hipStreamNonBlocking));
     HIPCHK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
@@ -2330,7 +2332,6 @@ int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, fl
     float w;
     h->quantile_ranks(n, klo, khi, w);
     if (ExtdmHandle::sampler_mw()) {
-      HIPCHK(hipMemsetAsync(h->sel, 0, sampler_sel_bytes(B), s));
       sampler_step_mw(s, x, eps, B, n, h->coefs, h->step_ctr, noise, 0, 0, 0, klo, khi, w, thresh_out, h->sel,
                       nullptr, 1);
     } else {
@@ -2367,10 +2368,11 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     float w;
     h->quantile_ranks(n, klo, khi, w);
     const bool mw = ExtdmHandle::sampler_mw();
+    // per-step thresholds [S][B] into the buffer extdm_record_thresholds set (tests)
+    REQUIRE(!h->thresh_rec || (int64_t)S * B <= h->thresh_cap, "threshold record buffer smaller than S x B");
+    float* thr = h->thresh_rec;
     if (mw) {
-      // the selection bins zeroed once; step 0's t set here, every later t (and the step counter)
-      // by the previous step's update launch
-      HIPCHK(hipMemsetAsync(h->sel, 0, sampler_sel_bytes(B), s));
+      // step 0's t set here, every later t (and the step counter) by the previous step's advance launch
       set_t_from_step(s, h->t_batch, B, h->coefs, h->step_ctr);
     }
     auto step = [&]() {
@@ -2378,10 +2380,10 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
       h->unet_step(B, out, cond_fea, h->eps_buf);
       if (mw) {
         sampler_step_mw(s, out, h->eps_buf, B, n, h->coefs, h->step_ctr, noise, seed, sample_base, round, klo, khi,
-                        w, nullptr, h->sel, h->t_batch, S);
+                        w, thr, h->sel, h->t_batch, S);
       } else {
         sampler_step(s, out, h->eps_buf, B, n, h->coefs, h->step_ctr, noise, seed, sample_base, round, klo, khi, w,
-                     nullptr);
+                     thr);
         incr_counter(s, h->step_ctr);
       }
     };
@@ -2406,6 +2408,15 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     REQUIRE(!h->x3_convs() || x3_range_read(s) == 0,
             "f16x3 precision: a conv input reached |v| >= 65504 during sampling; results are not fp32-accurate "
             "(create the handle with EXTDM_PRECISION_FP32)");
+  });
+}
+
+int extdm_record_thresholds(ExtdmHandle* h, float* buf, int64_t cap) {
+  return guarded([&] {
+    REQUIRE(h, "null handle");
+    REQUIRE(!buf || cap > 0, "record_thresholds: empty buffer");
+    h->thresh_rec = buf;
+    h->thresh_cap = buf ? cap : 0;
   });
 }
 

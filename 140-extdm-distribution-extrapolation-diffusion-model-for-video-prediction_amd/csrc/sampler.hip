@@ -132,7 +132,7 @@ __global__ __launch_bounds__(1024) void sampler_step_kernel(float* x, const floa
   // torch lerp (CPU): w < 0.5 ? a + w (b - a) : b - (b - a)(1 - w)
   float s = q_w < 0.5f ? vlo + q_w * (vhi - vlo) : vhi - (vhi - vlo) * (1.f - q_w);
   if (s < 1.f) s = 1.f;
-  if (thresh_out && threadIdx.x == 0) thresh_out[b] = s;
+  if (thresh_out && threadIdx.x == 0) thresh_out[(size_t)step * B + b] = s;
   const float* nb = noise ? noise + ((long)step * B + b) * n : nullptr;
   for (int e = threadIdx.x; e < n; e += blockDim.x) {
     const float xv = xb[e], ev = eb[e];
@@ -149,79 +149,106 @@ __global__ __launch_bounds__(1024) void sampler_step_kernel(float* x, const floa
   }
 }
 
-// ---- multi-workgroup form (round 5): the same step over (chunk, sample) workgroups ----
-// The one-workgroup-per-sample kernel above ran 4 radix passes x up to 2 selections over the whole
+// ---- multi-workgroup form: the same step over (chunk, sample) workgroups ----
+// The one-workgroup-per-sample kernel above runs 4 radix passes x up to 2 selections over the whole
 // sample in one workgroup: 4 of 256 CUs busy at UCF's B = 4 (2.6 ms per step) and 64 at BAIR's 64
-// (168 us). Here every pass is a launch over SCH-element chunks x samples: each workgroup counts its
-// chunk's |x0| bytes into LDS bins (filtered by the prefix chosen so far) and adds them into the
-// pass's global bins with integer atomics — exact counts, so the selected order statistics are the
-// same whatever the workgroup order (deterministic, bit-equal to the kernel above). Each workgroup
-// of the next pass re-derives the prefix and residual rank from the earlier passes' bins (a 256-bin
-// scan per selection, one wave each). The final launch derives the two order statistics, the
-// threshold, and updates its chunk; bins live in two sets by step parity, and the final launch
-// zeroes the other set (the previous step's, fully consumed) for the next step. One one-workgroup
-// launch then writes the next step's t and increments the step counter (sampler_advance_kernel,
-// replacing the set_t / incr pair).
+// (168 us). Here every pass is a launch over SCH-element chunks x samples. Each workgroup counts its
+// chunk's |x0| bytes (filtered by the prefix chosen so far) into LDS bins and STORES the chunk's
+// 256-bin histogram to its own slot hist[pass][b][chunk][sel][256] — no global atomics, no zeroing:
+// every slot is overwritten whole by one workgroup on every step. The next launch's workgroups sum
+// the sample's chunk histograms of the previous pass in a fixed order (integer sums: exact, so the
+// order statistics are those of the one-workgroup kernel whatever the workgroup order and placement)
+// and take the next radix digit. Chunk 0's workgroup of pass p stores the (prefix, mask, rank) state
+// after p digits for pass p + 1. The only cross-workgroup hand-offs are plain stores read by plain
+// loads in a LATER launch of the same stream — the kernel-boundary visibility every other producer /
+// consumer pair of the forward relies on. The final launch derives the two order
+// statistics and the threshold and updates its chunk; a one-workgroup launch then writes the next
+// step's t and increments the step counter (sampler_advance_kernel).
 constexpr int SCH = 4096;       // elements per workgroup
 constexpr int SNT = 256;        // threads per workgroup
-// selection workspace per sample: [2 sets][4 passes][2 selections][256 bins]
-constexpr int SEL_PER_SAMPLE = 2 * 4 * 2 * 256;
 
-// (prefix, mask, residual rank) of selection `sel` after `npass` passes, from the sample's bins
-// hb = [4 passes][2 sel][256] of the current set (wave-uniform results; called by a whole wave)
-__device__ void derive_sel(const unsigned* hb, int npass, int sel, unsigned rank0, unsigned& prefix, unsigned& mask,
-                           unsigned& rank) {
-  const int l = threadIdx.x & 63;
-  prefix = 0; mask = 0; rank = rank0;
-  for (int p = 0; p < npass; ++p) {
-    const int shift = 24 - 8 * p;
-    const unsigned* h = hb + (p * 2 + sel) * 256;
-    // device-scope atomic loads: the bins were built by other launches' device-scope atomics, and a
-    // plain load may hit a stale copy of the line in this XCD's L2 (kernel boundaries do not
-    // invalidate it; DESIGN.md §5 sampler note)
-    const unsigned h0 = __hip_atomic_load(h + 4 * l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned h1 = __hip_atomic_load(h + 4 * l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned h2 = __hip_atomic_load(h + 4 * l + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned h3 = __hip_atomic_load(h + 4 * l + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned tot = h0 + h1 + h2 + h3;
-    unsigned incl = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned v = __shfl_up(incl, o);
-      if (l >= o) incl += v;
-    }
-    const unsigned excl = incl - tot;
-    const bool mine = rank >= excl && rank < incl;
-    unsigned d = 4 * l, cum = excl;
-    if (rank >= cum + h0) { cum += h0; ++d;
-      if (rank >= cum + h1) { cum += h1; ++d;
-        if (rank >= cum + h2) { cum += h2; ++d; } } }
-    const unsigned long long bal = __ballot(mine);
-    const int src = bal ? __ffsll((long long)bal) - 1 : 0;
-    d = __shfl(d, src);
-    const unsigned nr = __shfl(rank - cum, src);
-    prefix |= d << shift;
-    mask |= 255u << shift;
-    rank = nr;
+struct SelLayout {
+  int B, nch;
+  __host__ __device__ size_t hist_words() const { return (size_t)4 * B * nch * 2 * 256; }
+  // histogram of (pass, sample, chunk, selection)
+  __host__ __device__ size_t hist(int p, int b, int ch, int sl) const {
+    return (((size_t)p * B + b) * nch + ch) * 512 + (size_t)sl * 256;
   }
+  // (prefix, mask, rank, -) after `p` digits (p = 1..3) of (sample, selection)
+  __host__ __device__ size_t state(int p, int b, int sl) const {
+    return hist_words() + (((size_t)p * B + b) * 2 + sl) * 4;
+  }
+  __host__ __device__ size_t words() const { return hist_words() + (size_t)4 * B * 2 * 4; }
+};
+
+// One radix digit of selection `sl` of sample b: the sum over the sample's chunks of pass `p`'s
+// histograms (fixed chunk order; lane l owns bins 4l..4l+3), then the bin holding residual rank
+// `rank`. Called by one whole wave; returns wave-uniform (digit, residual rank).
+__device__ void next_digit(const unsigned* ws, const SelLayout& L, int p, int b, int sl, unsigned rank,
+                           unsigned& digit, unsigned& nrank) {
+  const int l = threadIdx.x & 63;
+  uint4 s = make_uint4(0u, 0u, 0u, 0u);
+  for (int ch = 0; ch < L.nch; ++ch) {
+    const uint4 v = *reinterpret_cast<const uint4*>(ws + L.hist(p, b, ch, sl) + 4 * l);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const unsigned tot = s.x + s.y + s.z + s.w;
+  unsigned incl = tot;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned v = __shfl_up(incl, o);
+    if (l >= o) incl += v;
+  }
+  const unsigned excl = incl - tot;
+  const bool mine = rank >= excl && rank < incl;
+  unsigned d = 4 * l, cum = excl;
+  if (rank >= cum + s.x) { cum += s.x; ++d;
+    if (rank >= cum + s.y) { cum += s.y; ++d;
+      if (rank >= cum + s.z) { cum += s.z; ++d; } } }
+  const unsigned long long bal = __ballot(mine);
+  const int src = bal ? __ffsll((long long)bal) - 1 : 0;
+  digit = __shfl(d, src);
+  nrank = __shfl(rank - cum, src);
+}
+
+// (prefix, mask, residual rank) of selection sl after PASS digits: from the stored state after
+// PASS - 1 digits (written by the previous launch's chunk-0 workgroup) and pass PASS - 1's chunk
+// histograms. Whole wave; chunk 0's lane 0 stores it for the next launch when `store`.
+template <int PASS>
+__device__ void sel_state(unsigned* ws, const SelLayout& L, int b, int sl, unsigned rank0, bool store,
+                          unsigned& prefix, unsigned& mask, unsigned& rank) {
+  if (PASS == 0) { prefix = 0; mask = 0; rank = rank0; return; }
+  unsigned pp = 0, pm = 0, pr = rank0;
+  if (PASS > 1) {
+    const uint4 st = *reinterpret_cast<const uint4*>(ws + L.state(PASS - 1, b, sl));
+    pp = st.x; pm = st.y; pr = st.z;
+  }
+  unsigned d, nr;
+  next_digit(ws, L, PASS - 1, b, sl, pr, d, nr);
+  constexpr int shift = 24 - 8 * (PASS - 1);
+  prefix = pp | (d << shift);
+  mask = pm | (255u << shift);
+  rank = nr;
+  if (store && PASS < 4 && (threadIdx.x & 63) == 0)
+    *reinterpret_cast<uint4*>(ws + L.state(PASS, b, sl)) = make_uint4(prefix, mask, rank, 0u);
 }
 
 template <int PASS>
 __global__ __launch_bounds__(SNT) void radix_count_kernel(const float* x, const float* eps, int n,
                                                           const StepCoef* coefs, const int* step_ctr,
-                                                          unsigned* sel, int k_lo, int k_hi) {
+                                                          unsigned* ws, int k_lo, int k_hi) {
   __shared__ unsigned lh[2][256];
   __shared__ unsigned st[2][2];  // [sel][prefix, mask]
-  const int b = blockIdx.y;
+  const SelLayout L{(int)gridDim.y, (int)gridDim.x};
+  const int b = blockIdx.y, ch = blockIdx.x;
   const int step = *step_ctr;
   const StepCoef c = coefs[step];
-  unsigned* hb = sel + ((size_t)(step & 1) * gridDim.y + b) * (4 * 2 * 256);
   const int nsel = k_hi == k_lo ? 1 : 2;
   for (int i = threadIdx.x; i < 512; i += SNT) lh[i >> 8][i & 255] = 0;
   if (threadIdx.x < 64 * nsel) {
     const int sl = threadIdx.x >> 6;
     unsigned pf, mk, rk;
-    derive_sel(hb, PASS, sl, (unsigned)(sl ? k_hi : k_lo), pf, mk, rk);
+    sel_state<PASS>(ws, L, b, sl, (unsigned)(sl ? k_hi : k_lo), ch == 0, pf, mk, rk);
     if ((threadIdx.x & 63) == 0) { st[sl][0] = pf; st[sl][1] = mk; }
   }
   __syncthreads();
@@ -230,47 +257,43 @@ __global__ __launch_bounds__(SNT) void radix_count_kernel(const float* x, const 
   constexpr int shift = 24 - 8 * PASS;
   const float* xb = x + (long)b * n;
   const float* eb = eps + (long)b * n;
-  const int e0 = blockIdx.x * SCH, e1 = min(n, e0 + SCH);
+  const int e0 = ch * SCH, e1 = min(n, e0 + SCH);
   for (int e = e0 + threadIdx.x; e < e1; e += SNT) {
     const unsigned u = x0_bits(xb, eb, c, e);
     if ((u & m0) == p0) atomicAdd(&lh[0][(u >> shift) & 255u], 1u);
     if (nsel > 1 && (u & m1) == p1) atomicAdd(&lh[1][(u >> shift) & 255u], 1u);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 256 * nsel; i += SNT) {
-    const unsigned v = lh[i >> 8][i & 255];
-    if (v) atomicAdd(&hb[(PASS * 2 + (i >> 8)) * 256 + (i & 255)], v);
+  // the chunk's histograms, stored whole (zero bins included): 16 B per thread
+  for (int i = 4 * threadIdx.x; i < 256 * nsel; i += 4 * SNT) {
+    const int sl = i >> 8, j = i & 255;
+    *reinterpret_cast<uint4*>(ws + L.hist(PASS, b, ch, sl) + j) =
+        make_uint4(lh[sl][j], lh[sl][j + 1], lh[sl][j + 2], lh[sl][j + 3]);
   }
 }
 
 __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const float* eps, int n, const StepCoef* coefs,
-                                                            int* step_ctr, const float* noise, int B, uint64_t seed,
-                                                            int sample_base, int round, int k_lo, int k_hi, float q_w,
-                                                            float* thresh_out, unsigned* sel, int* t_next, int nsteps) {
+                                                            const int* step_ctr, const float* noise, int B,
+                                                            uint64_t seed, int sample_base, int round, int k_lo,
+                                                            int k_hi, float q_w, float* thresh_out, unsigned* ws) {
   __shared__ float vs[2];
+  const SelLayout L{(int)gridDim.y, (int)gridDim.x};
   const int b = blockIdx.y;
   const int step = *step_ctr;
   const StepCoef c = coefs[step];
-  const int set = step & 1;
-  const unsigned* hb = sel + ((size_t)set * gridDim.y + b) * (4 * 2 * 256);
   const int nsel = k_hi == k_lo ? 1 : 2;
   if (threadIdx.x < 64 * nsel) {
     const int sl = threadIdx.x >> 6;
     unsigned pf, mk, rk;
-    derive_sel(hb, 4, sl, (unsigned)(sl ? k_hi : k_lo), pf, mk, rk);
+    sel_state<4>(ws, L, b, sl, (unsigned)(sl ? k_hi : k_lo), false, pf, mk, rk);
     if ((threadIdx.x & 63) == 0) vs[sl] = __uint_as_float(pf);
   }
-  // the other set's bins of this sample: the previous step's, consumed; zeroed for the next step
-  // (each of the sample's chunk workgroups takes a share)
-  unsigned* ob = sel + ((size_t)(set ^ 1) * gridDim.y + b) * (4 * 2 * 256);
-  for (int i = blockIdx.x * SNT + threadIdx.x; i < 4 * 2 * 256; i += gridDim.x * SNT)
-    __hip_atomic_store(ob + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // at the atomics' coherence point
   __syncthreads();
   const float vlo = vs[0], vhi = nsel > 1 ? vs[1] : vs[0];
   // torch lerp (CPU): w < 0.5 ? a + w (b - a) : b - (b - a)(1 - w)
   float s = q_w < 0.5f ? vlo + q_w * (vhi - vlo) : vhi - (vhi - vlo) * (1.f - q_w);
   if (s < 1.f) s = 1.f;
-  if (thresh_out && blockIdx.x == 0 && threadIdx.x == 0) thresh_out[b] = s;
+  if (thresh_out && blockIdx.x == 0 && threadIdx.x == 0) thresh_out[(size_t)step * B + b] = s;
   float* xb = x + (long)b * n;
   const float* eb = eps + (long)b * n;
   const float* nb = noise ? noise + ((long)step * B + b) * n : nullptr;
@@ -313,11 +336,8 @@ __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const floa
   }
 }
 
-// t and the step counter for the next step (one workgroup, after the update launch). Folding this
-// into the update launch (its last workgroup, found by a global completion count) needed a
-// device-scope release fence in every workgroup before the count — on gfx950 a write-back of the
-// XCD's whole L2, issued by each of the B x n / 4096 workgroups: ~150 us per BAIR step at 128 clips;
-// without the fences the next step's kernels saw stale counters across XCDs (two-rank bench test).
+// t and the step counter for the next step (one workgroup, after the update launch: every
+// workgroup of this step has read the counter before it changes).
 __global__ __launch_bounds__(256) void sampler_advance_kernel(int* step_ctr, const StepCoef* coefs, int* t_next, int B,
                                                               int nsteps) {
   const int step = *step_ctr;
@@ -401,18 +421,20 @@ void sampler_step(hipStream_t s, float* x, const float* eps, int B, int n, const
                      sample_base, round, k_lo, k_hi, q_w, thresh_out);
 }
 
-size_t sampler_sel_bytes(int B) { return ((size_t)B * SEL_PER_SAMPLE + 4) * sizeof(unsigned); }
+size_t sampler_sel_bytes(int B, int n) {
+  return SelLayout{B, (n + SCH - 1) / SCH}.words() * sizeof(unsigned);
+}
 
 void sampler_step_mw(hipStream_t s, float* x, const float* eps, int B, int n, const StepCoef* coefs, int* step_ctr,
                      const float* noise, uint64_t seed, int sample_base, int round, int k_lo, int k_hi, float q_w,
-                     float* thresh_out, unsigned* sel, int* t_next, int nsteps) {
+                     float* thresh_out, unsigned* ws, int* t_next, int nsteps) {
   const dim3 grid((n + SCH - 1) / SCH, B);
-  hipLaunchKernelGGL(radix_count_kernel<0>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, sel, k_lo, k_hi);
-  hipLaunchKernelGGL(radix_count_kernel<1>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, sel, k_lo, k_hi);
-  hipLaunchKernelGGL(radix_count_kernel<2>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, sel, k_lo, k_hi);
-  hipLaunchKernelGGL(radix_count_kernel<3>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, sel, k_lo, k_hi);
+  hipLaunchKernelGGL(radix_count_kernel<0>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, ws, k_lo, k_hi);
+  hipLaunchKernelGGL(radix_count_kernel<1>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, ws, k_lo, k_hi);
+  hipLaunchKernelGGL(radix_count_kernel<2>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, ws, k_lo, k_hi);
+  hipLaunchKernelGGL(radix_count_kernel<3>, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, ws, k_lo, k_hi);
   hipLaunchKernelGGL(sampler_final_kernel, grid, dim3(SNT), 0, s, x, eps, n, coefs, step_ctr, noise, B, seed,
-                     sample_base, round, k_lo, k_hi, q_w, thresh_out, sel, t_next, nsteps);
+                     sample_base, round, k_lo, k_hi, q_w, thresh_out, ws);
   if (t_next) hipLaunchKernelGGL(sampler_advance_kernel, dim3(1), dim3(256), 0, s, step_ctr, coefs, t_next, B, nsteps);
 }
 

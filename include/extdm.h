@@ -114,6 +114,12 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
                  const float* x_cond, const float* cond_fea, const float* x_T, const float* noise, uint64_t seed,
                  int sample_base, int round, float* out, int use_graph, void* stream);
 
+/* Record the dynamic-threshold value s = max(1, quantile(|x0|, 0.9)) of every step and sample
+ * of later extdm_sample calls into buf[k * B + b] (device fp32, cap floats >= S x B; NULL
+ * stops recording). Verification hook for the captured-graph sampler (the threshold inside
+ * p_mean_variance, Diffusion.py:150-163); the step itself is unchanged. */
+int extdm_record_thresholds(ExtdmHandle* h, float* buf, int64_t cap);
+
 /* One sampler update in place on x given eps (the step-k coefficients). */
 int extdm_sampler_step(ExtdmHandle* h, int B, int sampler, int t, int t_next, float eta, float* x, const float* eps,
                        const float* noise, float* thresh_out, void* stream);

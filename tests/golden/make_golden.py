@@ -7,7 +7,8 @@ replaced by the stand-ins under tests/golden/shims/ (einops_exts, timm,
 skimage: import-only; rotary_embedding_torch: restatement of 0.8.3; cv2: the two
 OpenCV calls of calculate_ssim.py restated).
 
-Usage (build container only):  python tests/golden/make_golden.py [--variants|--lfae|--wrappers|--metrics|--e2e]
+Usage (build container only):  python tests/golden/make_golden.py
+    [--variants|--lfae|--wrappers|--metrics|--e2e|--ddpm1000|--bair-chain]
 """
 import importlib
 import json
@@ -220,6 +221,38 @@ def ddpm1000():
                 out[f'x_after_{i}'] = img.numpy()
                 print('ddpm1000 t', i, float(img.abs().max()), flush=True)
     np.savez_compressed(os.path.join(HERE, 'ddpm1000.npz'), **out)
+
+
+def bair_chain():
+    """A few DDPM steps at the metric's size (VERDICT r5 'Next round' item 2): the full BAIR u12
+    denoiser (dim 64, 2 -> 14, latent 32: n = 43 008 per sample), B = 4, t = 999 .. 996 through
+    the reference's own p_sample with its torch.randn stream (x_T, then one draw per step after
+    torch.manual_seed), x after every step, and each step's dynamic threshold
+    s = max(1, quantile(|x_recon|, 0.9)) restated from the reference's own p_mean_variance pieces
+    (predict_start_from_noise on the same net output; Diffusion.py:145-163)
+    (tests/golden/bair_chain.npz)."""
+    from tests.golden_inputs import BAIR_CHAIN
+    Unet3D, GaussianDiffusion, _ = import_reference()
+    cfg = CONFIGS['bair']
+    B, seed, times = BAIR_CHAIN['B'], BAIR_CHAIN['noise_seed'], BAIR_CHAIN['times']
+    _, _, cond, fea = unet_inputs(cfg, B=B, seed=BAIR_CHAIN['seed'])
+    net = build_ref_unet(Unet3D, cfg)
+    net.load_state_dict(make_sd(cfg), strict=True)
+    d = GaussianDiffusion(net, image_size=cfg.latent, num_frames=cfg.tc + cfg.tp, timesteps=1000,
+                          sampling_timesteps=1000, null_cond_prob=0.0)
+    torch.manual_seed(seed)
+    img = torch.randn((B, 3, cfg.tp, cfg.latent, cfg.latent))
+    out = {}
+    with torch.no_grad():
+        for i in times:
+            tt = torch.full((B,), i, dtype=torch.long)
+            eps = net(img, tt, cond, cond_fea=fea)
+            xr = d.predict_start_from_noise(img, t=tt, noise=eps)
+            out[f'thresh_{i}'] = torch.quantile(xr.reshape(B, -1).abs(), 0.9, dim=-1).clamp(min=1.).numpy()
+            img = d.p_sample(cond, img, fea, tt)
+            out[f'x_after_{i}'] = img.numpy()
+            print('bair_chain t', i, out[f'thresh_{i}'], flush=True)
+    np.savez_compressed(os.path.join(HERE, 'bair_chain.npz'), **out)
 
 
 def e2e():
@@ -464,6 +497,10 @@ def metrics():
 
 
 if __name__ == '__main__':
+    if '--bair-chain' in sys.argv:
+        torch.set_num_threads(8)
+        bair_chain()
+        sys.exit(0)
     if '--ddpm1000' in sys.argv:
         torch.set_num_threads(8)
         import_reference()

@@ -113,6 +113,18 @@ def ddpm1000_case():
 
 DDPM1000_SNAPS = [999, 900, 500, 100, 10, 0]  # x after the step at these t
 
+# DDPM steps at the metric's sample size (full BAIR u12, n = 43 008, B = 4; tests/golden/bair_chain.npz):
+# x_T and one torch.randn draw per step after torch.manual_seed(noise_seed), cond / fea from seed
+BAIR_CHAIN = {'B': 4, 'seed': 71, 'noise_seed': 72, 'times': [999, 998, 997, 996]}
+
+
+def bair_chain_noise(cfg, B=4, S=4, seed=72):
+    """The reference's RNG stream for BAIR_CHAIN: x_T, then one draw per p_sample."""
+    torch.manual_seed(seed)
+    shape = (B, 3, cfg.tp, cfg.latent, cfg.latent)
+    xT = torch.randn(shape)
+    return xT, torch.stack([torch.randn(shape) for _ in range(S)])
+
 
 def ddim_noise(shape, S=10):
     """The CPU noise stream one reference ddim_sample consumes after torch.manual_seed:

@@ -1,0 +1,130 @@
+"""GPU: the sampler at the metric's sample size (VERDICT r5 'Next round' items 1-2).
+
+Every other sampler test runs the reduced `small` config (n = 4 608: two 4 096-element chunks).
+Here the full BAIR u12 denoiser (dim 64, 2 -> 14, latent 32) gives n = 43 008 per sample: 11
+chunks x B workgroups per radix launch, spread over all eight XCDs, on the captured-graph path
+the bench runs (sampler.hip's multi-workgroup step; Diffusion.py:145-189).
+
+  thresholds (graph path, recorded per step) == the single-step entry's == torch.quantile of
+      the same x0 (CPU), bit for bit
+  graph chain == eager step-by-step replay, bit for bit
+  multi-workgroup form == one-workgroup-per-sample form (EXTDM_SAMPLER_1WG=1), bit for bit
+  x after each step vs the reference's own p_sample (tests/golden/bair_chain.npz) within the
+      fp32 contract; thresholds vs the reference's within fp32 rounding of x0
+  repeated runs and 2-way clip sharding (Philox noise keyed by global sample index) bit for bit
+"""
+import importlib
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from tests import parity_log
+from tests.golden_inputs import BAIR_CHAIN, CONFIGS, PKG, bair_chain_noise, unet_inputs
+from tests.sampler_run import bair_handle, graph_chain
+from tests.test_oracle_golden import load
+
+pytestmark = pytest.mark.gpu
+pkg = importlib.import_module(PKG)
+DEV = torch.device('cuda:0')
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_H = {}
+
+
+def handle(B):
+    if B not in _H:
+        _H[B] = bair_handle(B)
+    return _H[B]
+
+
+def chain_inputs():
+    cfg, B = CONFIGS['bair'], BAIR_CHAIN['B']
+    _, _, cond, fea = unet_inputs(cfg, B=B, seed=BAIR_CHAIN['seed'])
+    xT, noise = bair_chain_noise(cfg, B, len(BAIR_CHAIN['times']), BAIR_CHAIN['noise_seed'])
+    return cfg, B, BAIR_CHAIN['times'], cond, fea, xT, noise
+
+
+def test_bair_size_graph_thresholds_vs_quantile_eager_and_reference():
+    cfg, B, times, cond, fea, xT, noise = chain_inputs()
+    h = handle(B)
+    out, rec = graph_chain(h, B, times, cond, fea, xT, noise, DEV)
+    g = load('bair_chain.npz')
+    sch = pkg.schedule_buffers(1000)
+    x = xT.to(DEV).contiguous()
+    cd, fd = cond.to(DEV), fea.to(DEV)
+    for k, ti in enumerate(times):
+        tt = torch.full((B,), ti, dtype=torch.long, device=DEV)
+        eps = torch.empty_like(x)
+        h.unet_forward(x, tt, cd, fd, eps)
+        torch.cuda.synchronize()
+        # the kernel's x0: fp32 products and difference, no contraction (Diffusion.py:130-134)
+        x0 = sch['sqrt_recip_alphas_cumprod'][ti] * x.cpu() - sch['sqrt_recipm1_alphas_cumprod'][ti] * eps.cpu()
+        ref = torch.quantile(x0.reshape(B, -1).abs(), 0.9, dim=-1).clamp(min=1.0)
+        th = torch.full((B,), -1., device=DEV)
+        h.sampler_step(0, ti, 0, 0., x, eps, noise[k:k + 1].to(DEV).contiguous(), th)
+        torch.cuda.synchronize()
+        assert torch.equal(th.cpu(), ref), (ti, th.cpu(), ref)
+        assert torch.equal(rec[k], ref), (ti, rec[k], ref)
+        # against the reference's own chain (its fp32 eps differs from ours by ~1e-5 relative)
+        rel = float((rec[k] - torch.from_numpy(g[f'thresh_{ti}'])).abs().max() / rec[k].abs().max())
+        parity_log.check(rel, 1e-4, f'threshold rel t={ti}')
+        parity_log.check(np.abs(x.cpu().numpy() - g[f'x_after_{ti}']).max(), 1e-4, f'x after t={ti}')
+    assert torch.equal(out, x.cpu())
+
+
+def test_bair_size_one_workgroup_form_equals_multi_workgroup(tmp_path):
+    """The same graph chain in two helper processes, EXTDM_SAMPLER_1WG=0 and =1."""
+    res = {}
+    for form in ('0', '1'):
+        dump = tmp_path / f'form{form}.pt'
+        env = dict(os.environ, EXTDM_SAMPLER_1WG=form)
+        p = subprocess.run([sys.executable, os.path.join(REPO, 'tests', 'sampler_run.py'), '--out', str(dump)],
+                           cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-3000:]
+        res[form] = torch.load(dump, weights_only=True)
+    assert torch.equal(res['0']['thresh'], res['1']['thresh']), (res['0']['thresh'], res['1']['thresh'])
+    assert torch.equal(res['0']['out'], res['1']['out'])
+    # and the in-process chain of the test above (same inputs, this process's library state)
+    cfg, B, times, cond, fea, xT, noise = chain_inputs()
+    out, rec = graph_chain(handle(B), B, times, cond, fea, xT, noise, DEV)
+    assert torch.equal(rec, res['0']['thresh']) and torch.equal(out, res['0']['out'])
+
+
+def test_bair_size_repeatable_and_shard_invariant():
+    """16 clips, 6 DDPM steps with the Philox noise stream, graph path: two runs and two 8-clip
+    shards (sample_base 0 / 8) give the same videos and thresholds bit for bit (the property
+    bench.py's multi-rank path rests on)."""
+    cfg, B = CONFIGS['bair'], 16
+    _, _, cond, fea = unet_inputs(cfg, B=B, seed=73)
+    h = handle(B)
+    times = list(range(999, 993, -1))
+    S = len(times)
+    cd, fd = cond.to(DEV), fea.to(DEV)
+    outs, recs = [], []
+    for _ in range(2):
+        rec = torch.full((S * B,), -1., device=DEV)
+        h.record_thresholds(rec)
+        o = torch.empty((B, 3, cfg.tp, cfg.latent, cfg.latent), device=DEV)
+        h.sample(0, times, None, 0., cd, fd, o, seed=99, sample_base=0, use_graph=True)
+        torch.cuda.synchronize()
+        outs.append(o.cpu())
+        recs.append(rec.cpu().view(S, B))
+    h.record_thresholds(None)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(recs[0], recs[1])
+    assert bool((recs[0] > 1).all())
+    parts, prec = [], []
+    for base in (0, 8):
+        rec = torch.full((S * 8,), -1., device=DEV)
+        h.record_thresholds(rec)
+        o = torch.empty((8, 3, cfg.tp, cfg.latent, cfg.latent), device=DEV)
+        h.sample(0, times, None, 0., cd[base:base + 8].contiguous(), fd[base:base + 8].contiguous(), o, seed=99,
+                 sample_base=base, use_graph=True)
+        torch.cuda.synchronize()
+        parts.append(o.cpu())
+        prec.append(rec.cpu().view(S, 8))
+    h.record_thresholds(None)
+    assert torch.equal(torch.cat(prec, dim=1), recs[0])
+    assert torch.equal(torch.cat(parts), outs[0])
