@@ -32,7 +32,12 @@ PER_FILE = {'stw_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA, 'stw64_x3.hip': ['
             'attn_core.hip': VGPR_MFMA,
             # the scaled-lo gather split as v_mul + v_fma_mixlo per value (SLP packed it into
             # v_pk_mul / v_pk_fma_f32 with the hi converted back: ~9 VALU per pair)
-            'xpath_x3.hip': ['-fno-slp-vectorize']}
+            'xpath_x3.hip': ['-fno-slp-vectorize'],
+            # the SLP-packed form of the sampler's four-wide update (v_pk_mul_f32 on SGPR pairs
+            # around the IEEE divisions) returned wrong values in 16-lane groups of one
+            # component in ~9 % of launches while a second process ran on the GPU; scalar
+            # fp32: 0 in 175 000 (tests/test_gpu_sampler.py)
+            'sampler.hip': ['-fno-slp-vectorize']}
 OPT = {}
 
 

@@ -2201,7 +2201,11 @@ int guarded(F&& f) {
 
 namespace extdm {
 static thread_local std::string g_noted_kernel;
+// kernel-name notes are formatted only inside extdm_bench_layer (NoteScope): the forward's
+// launchers call note_kernel on every launch
+static thread_local bool g_note_on = false;
 void note_kernel(const char* fmt, ...) {
+  if (!g_note_on) return;
   char buf[256];
   va_list ap;
   va_start(ap, fmt);
@@ -2210,6 +2214,10 @@ void note_kernel(const char* fmt, ...) {
   g_noted_kernel = buf;
 }
 const char* noted_kernel() { return g_noted_kernel.c_str(); }
+struct NoteScope {
+  NoteScope() { g_note_on = true; g_noted_kernel.clear(); }
+  ~NoteScope() { g_note_on = false; }
+};
 }  // namespace extdm
 
 extern "C" {
@@ -2310,6 +2318,7 @@ int extdm_unet_forward(ExtdmHandle* h, int B, const float* x, const int64_t* t, 
     REQUIRE(B >= 1 && B <= h->cfg.max_batch, "batch exceeds max_batch");
     HIPCHK(hipSetDevice(h->cfg.device));
     h->s = reinterpret_cast<hipStream_t>(stream);
+    h->bench_stage = 0;
     t_to_int(h->s, t, h->t_batch, B);
     h->unet_forward(B, x, cond, fea, out);
     HIPCHK(hipGetLastError());
@@ -2352,6 +2361,7 @@ int extdm_sample(ExtdmHandle* h, int B, int sampler, int S, const int* times, co
     hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
     hipStream_t s = h->work;
     h->s = s;
+    h->bench_stage = 0;
     HIPCHK(hipEventRecord(h->ev_in, caller));
     HIPCHK(hipStreamWaitEvent(s, h->ev_in, 0));
     h->ensure_coefs(S);
@@ -2461,6 +2471,12 @@ int extdm_bench_layer(ExtdmHandle* h, int B, int layer, int iters, float* ms_out
     hipStream_t s = h->work;
     h->s = s;
     Scope sc(h->arena);
+    NoteScope notes;
+    // bench_stage makes stw() / temporal() skip launches: back to 0 however this call ends
+    struct StageReset {
+      ExtdmHandle* h;
+      ~StageReset() { h->bench_stage = 0; }
+    } stage_reset{h};
     const int T = h->frames(), L = h->cfg.latent;
     // layer 0: init_conv, conv3d (1,7,7) channels -> dim over (B, T, L, L) (u12:913, 1041),
     // input as the forward issues it: two sources (x-branch, cond_fea branch).

@@ -15,6 +15,12 @@
 // batch is sharded over ranks.
 #include "kernels.h"
 
+// EXTDM_SAMPLER_DEBUG (diagnostic builds only): the multi-workgroup update records every chunk
+// workgroup's threshold, thresh_out[(step B + b) nch + chunk]
+#ifndef EXTDM_SAMPLER_DEBUG
+#define EXTDM_SAMPLER_DEBUG 0
+#endif
+
 namespace extdm {
 
 namespace {
@@ -293,7 +299,11 @@ __global__ __launch_bounds__(SNT) void sampler_final_kernel(float* x, const floa
   // torch lerp (CPU): w < 0.5 ? a + w (b - a) : b - (b - a)(1 - w)
   float s = q_w < 0.5f ? vlo + q_w * (vhi - vlo) : vhi - (vhi - vlo) * (1.f - q_w);
   if (s < 1.f) s = 1.f;
+#if EXTDM_SAMPLER_DEBUG
+  if (thresh_out && threadIdx.x == 0) thresh_out[((size_t)step * B + b) * gridDim.x + blockIdx.x] = s;
+#else
   if (thresh_out && blockIdx.x == 0 && threadIdx.x == 0) thresh_out[(size_t)step * B + b] = s;
+#endif
   float* xb = x + (long)b * n;
   const float* eb = eps + (long)b * n;
   const float* nb = noise ? noise + ((long)step * B + b) * n : nullptr;

@@ -14,6 +14,7 @@ the bench runs (sampler.hip's multi-workgroup step; Diffusion.py:145-189).
   repeated runs and 2-way clip sharding (Philox noise keyed by global sample index) bit for bit
 """
 import importlib
+import json
 import os
 import subprocess
 import sys
@@ -128,3 +129,22 @@ def test_bair_size_repeatable_and_shard_invariant():
     h.record_thresholds(None)
     assert torch.equal(torch.cat(prec, dim=1), recs[0])
     assert torch.equal(torch.cat(parts), outs[0])
+
+
+def test_sampler_bitwise_stable_beside_a_second_gpu_process(tmp_path):
+    """Two processes on the GPU at once (the bench's gloo rehearsal runs two ranks on one card):
+    one repeats extdm_sampler_step on fixed inputs, the other whole sampling calls; every repeat
+    must equal the first bit for bit. hipcc's SLP-packed sampler update failed this in ~9 % of the
+    step repeats (16-lane groups of one component wrong, thresholds right: DESIGN.md §4.2)."""
+    sync = str(tmp_path / 'go')
+    procs = [subprocess.Popen([sys.executable, os.path.join(REPO, 'tests', 'contention_run.py'), '--mode', m,
+                               '--seconds', '8', '--sync', sync], cwd=REPO, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for m in ('step', 'sample')]
+    res = []
+    for p in procs:
+        out, err = p.communicate(timeout=300)
+        assert p.returncode == 0, err[-3000:]
+        res.append(json.loads([l for l in out.splitlines() if l.startswith('{')][-1]))
+    for r in res:
+        assert r['repeats'] > 10, r
+        assert r['mismatches'] == 0, r
