@@ -365,9 +365,15 @@ struct NoisePoolArgs {
   int T, L, F, LP;
   float* out; long ob, oc, ot; int Cout;
   const _Float16* w; const float* rscale; const float* bias;
+  const float* add; long ab, ac, at;  // conv7c3 only: residual added in the epilogue
 };
 bool noise_pool_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
                            const float* bias);
+// A plain (1,7,7) 'same' conv of the 3-channel x (ada_u22 / wo_ref init_conv x-branch, the cond_fea
+// branch hoisted into `add`): out = W * x + bias + add, from the zero-padded copy (xpad_forward), the
+// weights packed like noise_pool's (Pconv7c3); L a multiple of 32, Cout a multiple of 64
+bool conv7c3_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
+                        const float* bias, const View* add);
 bool conv_gemm_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                           int stride, int pad, const ConvEpi& epi);
 void cross_attention(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,

@@ -524,6 +524,72 @@ __global__ __launch_bounds__(256) void temporal_prologue_kernel(const float* x, 
   }
 }
 
+// The same prologue with a pixel's channels split over G thread groups (PX pixels per workgroup;
+// each pass's per-group double partials summed in group order): for the deep levels, where one
+// thread per pixel left a launch with a few workgroups walking every channel five times
+// (Cityscapes: 448 pixels, two workgroups, 212 us per launch).
+template <int PX, int G>
+__global__ __launch_bounds__(PX * G) void temporal_prologue_grp_kernel(const float* x, long sb, long sc, long st, int C,
+                                                                       int T, int HW, int B, const float* gamma,
+                                                                       const float* lw, const float* lb, float* z,
+                                                                       long zsb, long zsc, long zst, float* r, long rsb,
+                                                                       long rsc, long rst) {
+  __shared__ double red[G][PX];
+  const int px = threadIdx.x % PX, grp = threadIdx.x / PX;
+  const long idx = (long)blockIdx.x * PX + px;
+  const long npix = (long)B * T * HW;
+  const bool ok = idx < npix;
+  const long id2 = ok ? idx : 0;
+  const int hw = (int)(id2 % HW);
+  const int t = (int)((id2 / HW) % T);
+  const int b = (int)(id2 / ((long)HW * T));
+  const float* xp = x + (long)b * sb + (long)t * st + hw;
+  // the pixel's total of the groups' partials, in group order (every thread of the pixel)
+  auto total = [&](double v) {
+    red[grp][px] = v;
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < G; ++i) s += red[i][px];
+    __syncthreads();
+    return s;
+  };
+  double s = 0.0;
+  if (ok)
+    for (int c = grp; c < C; c += G) s += xp[(long)c * sc];
+  const double mean = total(s) / C;
+  const float m = (float)mean;
+  double v2 = 0.0;
+  if (ok)
+    for (int c = grp; c < C; c += G) {
+      const double d = (double)xp[(long)c * sc] - mean;
+      v2 += d * d;
+    }
+  const float den = sqrtf((float)(total(v2) / C) + 1e-5f);
+  // y = chanLN(x) * gamma ; moments of y
+  double sy = 0.0;
+  if (ok)
+    for (int c = grp; c < C; c += G) sy += (double)((xp[(long)c * sc] - m) / den * gamma[c]);
+  const double my = total(sy) / C;
+  double vy = 0.0;
+  if (ok)
+    for (int c = grp; c < C; c += G) {
+      const double d = (double)((xp[(long)c * sc] - m) / den * gamma[c]) - my;
+      vy += d * d;
+    }
+  const float rstd2 = 1.0f / sqrtf((float)(total(vy) / C) + 1e-5f);
+  if (!ok) return;
+  const float m2 = (float)my;
+  float* zp = z + (long)b * zsb + (long)t * zst + hw;
+  float* rp = r + (long)b * rsb + (long)t * rst + hw;
+  for (int c = grp; c < C; c += G) {
+    const float xv = xp[(long)c * sc];
+    const float y = (xv - m) / den * gamma[c];
+    zp[(long)c * zsc] = (y - m2) * rstd2 * lw[c] + lb[c];
+    rp[(long)c * rsc] = xv + y;
+  }
+}
+
 // ---------------- layout / resampling ----------------
 __global__ __launch_bounds__(256) void copy_kernel(float* d, long dsb, long dsc, long dst_, const float* s,
                                                    long ssb, long ssc, long sst, int C, int T, int HW, long total) {
@@ -848,8 +914,16 @@ void channel_ln(hipStream_t s, const View& out, const View& in0, const View* in1
 void temporal_prologue(hipStream_t s, const View& x, const float* gamma, const float* lw, const float* lb,
                        const View& z, const View& r) {
   const long npix = (long)x.B * x.T * x.HW();
-  hipLaunchKernelGGL(temporal_prologue_kernel, dim3(nblk(npix)), dim3(256), 0, s, x.p, x.sb, x.sc, x.st, x.C, x.T,
-                     x.HW(), x.B, gamma, lw, lb, z.p, z.sb, z.sc, z.st, r.p, r.sb, r.sc, r.st);
+  // one thread per pixel where that fills the chip (256-wide coalesced channel planes), else the
+  // channels split over 16 groups of 16 pixels
+  if (npix >= 256L * 1024) {
+    hipLaunchKernelGGL(temporal_prologue_kernel, dim3(nblk(npix)), dim3(256), 0, s, x.p, x.sb, x.sc, x.st, x.C, x.T,
+                       x.HW(), x.B, gamma, lw, lb, z.p, z.sb, z.sc, z.st, r.p, r.sb, r.sc, r.st);
+  } else {
+    hipLaunchKernelGGL((temporal_prologue_grp_kernel<16, 16>), dim3((unsigned)((npix + 15) / 16)), dim3(256), 0, s, x.p,
+                       x.sb, x.sc, x.st, x.C, x.T, x.HW(), x.B, gamma, lw, lb, z.p, z.sb, z.sc, z.st, r.p, r.sb, r.sc,
+                       r.st);
+  }
 }
 
 void copy_view(hipStream_t s, const View& d, const View& src) {

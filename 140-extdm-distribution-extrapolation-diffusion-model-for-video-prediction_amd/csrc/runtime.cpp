@@ -460,13 +460,30 @@ struct ExtdmHandle {
   // init_noise_conv for the fused conv + maxpool kernel (noise_pool_x3_kernel): A fragments
   // [kstep = (ci, row pair)][m32][hi|lo][lane][8], k = 8*(lane >> 5) + e -> (dy = 2*pair +
   // (lane >> 5), dx = e), zero for dy or dx = 7; rows scaled by 2^s(m).
-  XPathW npw;
-  bool noise_pool_ready = false;
+  XPathW npw, c7w;
+  bool noise_pool_ready = false, c7_ready = false;
   const XPathW& Pnoise_pool() {
-    if (noise_pool_ready) return npw;
-    const HostTensor& wn = H("init_noise_conv.weight");  // [Cm][3][1][7][7]
+    if (!noise_pool_ready) npw = pack_conv7c3(H("init_noise_conv.weight"), "init_noise_conv");
+    noise_pool_ready = true;
+    return npw;
+  }
+  // init_conv's x half (init_conv.weight#x, ada_u22 / wo_ref) in the same layout (conv7c3_x3_kernel)
+  const XPathW& Pconv7c3() {
+    if (!c7_ready) {
+      split_init_conv(3);
+      c7w = pack_conv7c3(H("init_conv.weight#x"), "init_conv x-branch");
+    }
+    c7_ready = true;
+    return c7w;
+  }
+  bool conv7c3_on(const View& out) const {
+    static const bool off = [] { const char* v = getenv("EXTDM_NO_C7"); return v && v[0] && v[0] != '0'; }();
+    return !off && x3_convs() && out.H % 32 == 0 && out.W == out.H && out.C % 64 == 0;
+  }
+  XPathW pack_conv7c3(const HostTensor& wn, const char* what) {  // [Cm][3][1][7][7]
     const int Cm = (int)wn.shape[0], M32 = (Cm + 31) / 32;
-    REQUIRE(wn.shape[1] == 3 && wn.shape.back() == 7, "init_noise_conv: expected a 3 -> C (1,7,7) conv");
+    REQUIRE(wn.shape[1] == 3 && wn.shape.back() == 7, std::string(what) + ": expected a 3 -> C (1,7,7) conv");
+    XPathW pw;
     std::vector<_Float16> g((size_t)12 * M32 * 1024, (_Float16)0.f);
     std::vector<float> rs(M32 * 32, 0.f);
     for (int m = 0; m < Cm; ++m) {
@@ -486,12 +503,11 @@ struct ExtdmHandle {
             g[base + 512 + lane * 8 + dx] = (_Float16)(v - (float)hi);
           }
     }
-    npw.w = dmalloc(g.size() * sizeof(_Float16));
-    HIPCHK(hipMemcpy(npw.w, g.data(), g.size() * sizeof(_Float16), hipMemcpyHostToDevice));
-    npw.rs = dmalloc(rs.size() * sizeof(float));
-    HIPCHK(hipMemcpy(npw.rs, rs.data(), rs.size() * sizeof(float), hipMemcpyHostToDevice));
-    noise_pool_ready = true;
-    return npw;
+    pw.w = dmalloc(g.size() * sizeof(_Float16));
+    HIPCHK(hipMemcpy(pw.w, g.data(), g.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    pw.rs = dmalloc(rs.size() * sizeof(float));
+    HIPCHK(hipMemcpy(pw.rs, rs.data(), rs.size() * sizeof(float), hipMemcpyHostToDevice));
+    return pw;
   }
   bool noise_pool_enabled() const {
     return xpath_enabled() && cfg.arch == EXTDM_ARCH_U12 && cfg.latent <= 32 && cfg.latent % 2 == 0;
@@ -1490,7 +1506,15 @@ struct ExtdmHandle {
       View rp = r.frames(tc, tp);
       const bool hoist = fea_hoist_on();
       const View fr = hoist ? with_batch(fr_all, B) : View{};
-      if (hoist && (arch == EXTDM_ARCH_WO_REF || arch == EXTDM_ARCH_ADA_U22)) {
+      if (hoist && (arch == EXTDM_ARCH_WO_REF || arch == EXTDM_ARCH_ADA_U22) && conv7c3_on(rp)) {
+        // the 3-channel 7x7 x-branch on f16x3 MFMA from the zero-padded copy, + cond_fea branch + bias
+        const XPathW& cw = Pconv7c3();
+        View xpad = alloc_cf(B, 3, tp, xpad_size(L), xpad_size(L));
+        if (!plan) {
+          xpad_forward(s, xpad, vx);
+          REQUIRE(conv7c3_x3_forward(s, rp, xpad, cw.w, cw.rs, nullptr, &fr), "init_conv x-branch launch rejected");
+        }
+      } else if (hoist && (arch == EXTDM_ARCH_WO_REF || arch == EXTDM_ARCH_ADA_U22)) {
         split_init_conv(3);
         conv(rp, vx, nullptr, P("init_conv.weight#x"), 1, 3, nullptr, &fr);  // + cond_fea branch + bias
       } else if (arch == EXTDM_ARCH_WO_REF) {

@@ -272,9 +272,95 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void n
     }
 }
 
+// A plain (1,7,7) conv of the 3-channel x (ada_u22 / wo_ref init_conv x-branch; the reference
+// convolves cat(x, cond_fea) at once, ada_u22:1188-1190, wo_ref:911-921, and the cond_fea half is
+// hoisted out of the step into `add`): noise_pool's k-loop (K = 3 ch x 4 row pairs x 8 columns, 7
+// used; lane half h takes row 2 dyp + h) over 32-column tiles, no pool. A wave owns two output
+// rows x 32 columns of one frame and 64 output channels; each store instruction writes two whole
+// 128-B row segments (columns of one channel row, lanes 0-31 and 32-63 four channels apart).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv7c3_x3_kernel(NoisePoolArgs a) {
+  constexpr int MW = 2;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lc = lane & 31, h = lane >> 5;
+  const int L = a.L, nct = L / 32, Lh = L / 2;
+  const int nmq = a.Cout / (32 * MW);
+  const int unit = blockIdx.x * 4 + wave;  // (frame, row pair, column tile, m-group)
+  if (unit >= a.F * Lh * nct * nmq) return;
+  const int mq = unit % nmq, u2 = unit / nmq;
+  const int ct = u2 % nct, rp = u2 / nct;
+  const int f = rp / Lh, yp = rp - f * Lh;
+  const int b = f / a.T, t = f - b * a.T;
+  const int col = ct * 32 + lc;
+  // padded copy (x at (6, 6)): output (y, c) reads rows y + 3 .. y + 9, columns c + 3 .. c + 10
+  const unsigned* xf = reinterpret_cast<const unsigned*>(a.x) + (long)b * a.xb + (long)t * a.xt +
+                       (long)(2 * yp + 3) * a.LP + col + 3;
+  f32x16 acc[MW][2];
+#pragma unroll
+  for (int m = 0; m < MW; ++m)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[m][nt][r] = 0.f;
+  const _Float16* wq = a.w + (long)mq * MW * 1024 + lane * 8;
+  const int M32 = a.Cout / 32;
+#pragma unroll 2
+  for (int ks = 0; ks < 12; ++ks) {
+    const int ci = ks / 4, dy = 2 * (ks % 4) + h;
+    h8 ah[MW], al[MW];
+#pragma unroll
+    for (int m = 0; m < MW; ++m) {
+      const _Float16* ap = wq + (long)(ks * M32 + m) * 1024;
+      ah[m] = *reinterpret_cast<const h8*>(ap);
+      al[m] = *reinterpret_cast<const h8*>(ap + 512);
+    }
+    h8 bh[2], bl[2];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) gather8p(xf + (long)ci * a.xc + (nt + dy) * a.LP, bh[nt], bl[nt]);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int m = 0; m < MW; ++m) acc[m][nt] = mma3(ah[m], al[m], bh[nt], bl[nt], acc[m][nt]);
+  }
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const long pix = (long)(2 * yp + nt) * L + col;
+    float* of = a.out + (long)b * a.ob + (long)t * a.ot + pix;
+    const float* ad = a.add ? a.add + (long)b * a.ab + (long)t * a.at + pix : nullptr;
+#pragma unroll
+    for (int m = 0; m < MW; ++m)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (mq * MW + m) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float v = acc[m][nt][r] * a.rscale[row];
+        if (a.bias) v += a.bias[row];
+        if (ad) v += ad[(long)row * a.ac];
+        of[(long)row * a.oc] = v;
+      }
+  }
+}
+
 }  // namespace
 
 int xpad_size(int L) { return (L + 16 + 7) & ~7; }
+
+// x: the zero-padded copy (xpad_forward; LP = x.W, the latent L = out.H)
+bool conv7c3_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
+                        const float* bias, const View* add) {
+  const int L = out.H;
+  if (x.C != 3 || x.W != x.H || x.W != xpad_size(L) || x.st != (long)x.W * x.H || out.W != L || L % 32 != 0 ||
+      out.T != x.T || out.B != x.B || out.C % 64 != 0)
+    return false;
+  if (add && (add->B != out.B || add->C != out.C || add->T != out.T || add->H != L || add->W != L)) return false;
+  NoisePoolArgs a{};
+  a.x = x.p; a.xb = x.sb; a.xc = x.sc; a.xt = x.st; a.LP = x.W;
+  a.T = x.T; a.L = L; a.F = x.B * x.T;
+  a.out = out.p; a.ob = out.sb; a.oc = out.sc; a.ot = out.st; a.Cout = out.C;
+  a.w = reinterpret_cast<const _Float16*>(w); a.rscale = rscale; a.bias = bias;
+  if (add) { a.add = add->p; a.ab = add->sb; a.ac = add->sc; a.at = add->st; }
+  const long units = (long)a.F * (L / 2) * (L / 32) * (out.C / 64);
+  note_kernel("conv7c3_x3_kernel");
+  hipLaunchKernelGGL(conv7c3_x3_kernel, dim3((unsigned)((units + 3) / 4)), dim3(256), 0, s, a);
+  return true;
+}
 
 void xpad_forward(hipStream_t s, const View& xpad, const View& x) {
   const long n = (long)x.B * 3 * x.T * xpad.H * xpad.W;
