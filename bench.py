@@ -211,6 +211,76 @@ def synthetic_clips(B, tc, S, seed):
     return torch.from_numpy(rng.random((B, 3, tc, S, S), dtype=np.float32))
 
 
+CONFIG_NAMES = {'bair': 'BAIR 64x64 ch3', 'kth': 'KTH 64x64 ch1 (as 3 ch)', 'cityscapes': 'Cityscapes 128x128 ch3',
+                'ucf': 'UCF-101 256x256 ch3', 'smmnist': 'SMMNIST 64x64 ch1 (as 3 ch)'}
+
+
+def layer_what(layer, u, shapes):
+    return _layer_what(layer, u, shapes) or None
+
+
+def _layer_what(layer, u, shapes):
+    """What bench layer `layer` (runtime.cpp extdm_bench_layer) runs for denoiser config `u`
+    (spec.UnetConfig), with the operand shapes read from the denoiser's state_dict (`shapes`:
+    name -> shape); None where the layer does not exist in this denoiser."""
+    T, L, fs, d0 = u.frames, u.latent, u.fea_size, u.dim
+    win = 'x'.join(str(min(w, e)) for w, e in zip(u.window, (T, L, L)))
+    heads = f'{u.heads} heads x {u.dim_head}'
+
+    def sh(name):
+        return shapes.get(name)
+    if layer == 0:
+        if u.short == 'u12':
+            return (f'init_conv cond_fea branch, phase-composed: 2 row parities x 2 column phases, 1x5x5 over the '
+                    f'{fs}x{fs} map, {u.fea_ch} -> {d0} ch, {u.tp} frames')
+        w = sh('init_conv.weight')
+        return w and f'init_conv {w[1]} -> {w[0]} ch 1x7x7 over {T} frames of {L}x{L} px'
+    if layer == 11:
+        return (f'init_conv cond_fea branch edge corrections (2 line launches K = 5 x {u.fea_ch} + corners)'
+                if u.short == 'u12' else None)
+    if layer in (1, 5):
+        w = sh('downs.0.0.block2.proj.weight')
+        how = 'fp32 input staged' if layer == 1 else 'pre-split operand by LDS-DMA'
+        blk = 'block1-shape' if layer == 1 else 'block2'
+        return w and f'level-0 ResnetBlock {blk} conv {w[1]}->{w[0]} 1x3x3 at {L}x{L} px, {T} frames, {how}'
+    if layer == 6:
+        return (f'level-0 shifted-window attention (STW, C {d0}, {win} windows, {heads}), fused '
+                f'LN/qkv/RoPE/softmax/PV/proj')
+    if layer == 7:
+        return f'init_temporal_attn (C {d0}, {T} frames, {heads})'
+    if layer == 8:
+        return (f'TrajWarp cross-attention core ({u.tp * fs * fs} queries x {u.tc * fs * fs} keys, 8 heads)'
+                if u.short == 'u12' else None)
+    if layer == 4:
+        w = sh('ups.3.0.res_conv.weight')
+        return w and f'level-0 res_conv {w[1]}->{w[0]} 1x1x1 at {L}x{L} px, {T} frames'
+    if layer == 9:
+        return f'init_conv x-branch as one composed 13x13 conv 3->{d0}, K = 3x169' if u.short in ('u12', 'ada') else None
+    if layer == 10:
+        w = sh('init_noise_conv.weight')
+        return w and u.short == 'u12' and f'init_noise_conv 3->{w[0]} 1x7x7 + MaxPool(1,2,2), K = 3x49'
+    if layer == 12:
+        w = sh('init_traj.cross_att.linear_q.weight')
+        return w and f'TrajWarp linear_q {w[1]}->{w[0]} 1x1 + ReLU over {u.tp} x {fs}x{fs} px, weights register-resident (pw_x3)'
+    if layer == 13:
+        w = sh('downs.2.4.Tmodulator.weight')
+        return w and (f'level-2 MotionAdaptor Tmodulator, 1x1 over (T C) = {w[1]} -> {w[0]} channels of '
+                      f'{L // 4}x{L // 4} px')
+    if layer in (14, 16):
+        return f"{'the level-0 STW layer' if layer == 14 else 'init_temporal_attn'}'s qkv 1x1 conv"
+    if layer in (15, 17):
+        return f"{'the level-0 STW layer' if layer == 15 else 'init_temporal_attn'}'s proj 1x1 conv + residual"
+    return None
+
+
+def metric_label(config, meta_metric, sampler, name, tc, total_pred, baseline):
+    """BASELINE.json's metric for the BAIR line; the other workloads' lines name their own."""
+    if config == 'bair':
+        return meta_metric
+    return (f'predicted frames/sec/GPU ({sampler}) {name} {tc}->{total_pred} — bench line of {baseline}, '
+            f'not the headline metric')
+
+
 class NativeWorkload:
     """The product path: FlowDiffusion + autoregressive_sample on the HIP library, for one of
     the BASELINE workloads (WORKLOADS[args.config])."""
@@ -270,8 +340,7 @@ class NativeWorkload:
         a, B, w = self.args, self.args.batch, self.w
         T = self.fd.diffusion.num_timesteps
         sampler = f'DDPM {T}' if a.sampling_steps >= T else f'DDIM {a.sampling_steps} (of {T})'
-        names = {'bair': 'BAIR 64x64 ch3', 'kth': 'KTH 64x64 ch1 (as 3 ch)', 'cityscapes': 'Cityscapes 128x128 ch3',
-                 'ucf': 'UCF-101 256x256 ch3', 'smmnist': 'SMMNIST 64x64 ch1 (as 3 ch)'}
+        names = CONFIG_NAMES
         unet = self.fd.unet.__class__.__name__
         return {
             'dtype': {'fp32': 'fp32', 'f16x3': 'fp32 (f16x3 split-MFMA convs + attention, fp32 accumulate)',
@@ -329,8 +398,8 @@ class NativeWorkload:
     # per-lane attention kernels (stw64_x3, attn_x3 without its tile path: 4-B loads per lane).
     WIDE_READS = {0, 1, 4, 5, 8, 11, 12, 13}
     # HBM-bound entries: (input + output channels, spatial size per frame, frames) of the algorithmic bytes
-    HBM_BYTES = {4: lambda u, T: (128 + 64, u.latent ** 2, T),
-                 12: lambda u, T: (256 + 256, u.fea_size ** 2, u.tp)}
+    HBM_BYTES = {4: lambda u, T, sh: (sum(sh['ups.3.0.res_conv.weight'][:2]), u.latent ** 2, T),
+                 12: lambda u, T, sh: (sum(sh['init_traj.cross_att.linear_q.weight'][:2]), u.fea_size ** 2, u.tp)}
 
     @staticmethod
     def wide_reads(layer, kname):
@@ -369,7 +438,7 @@ class NativeWorkload:
         """Share of an attention layer's FLOPs in QK^T / PV: per token 4 N hid of 2 C 3 hid + 4 N hid
         + 2 hid C (N = window tokens at level 0, or frames) = 4 N / (8 C + 4 N)."""
         u = self.fd.unet.ucfg
-        T = self.tc + self.tp
+        T = u.frames
         C = u.dim
         if layer in (6, 14, 15):
             ws = list(u.window)
@@ -382,13 +451,20 @@ class NativeWorkload:
         return 4.0 * N / (8.0 * C + 4.0 * N)
 
     def layer_ids(self):
-        """(id, bound, static template or None, what) in report order: this workload's lead first."""
+        """(id, bound, static template or None, what) in report order: this workload's lead first;
+        `what` from this denoiser's own config and weight shapes (layer_what), layers it lacks left out."""
         layers = list(self.LAYERS)
         lead = self.w.get('lead')
         if lead:
             i = next(k for k, e in enumerate(layers) if e[0] == lead[0])
             layers = [(lead[0], layers[i][1], None, lead[1])] + layers[:i] + layers[i + 1:]
-        return layers
+        shapes = {k: tuple(v.shape) for k, v in self.fd.unet.state_dict().items()}
+        out = []
+        for lid, bound, kname, _ in layers:
+            what = layer_what(lid, self.fd.unet.ucfg, shapes)
+            if what:
+                out.append((lid, bound, kname, what))
+        return out
 
     def roofline(self):
         """Per kernel, timed over 20 launches of the exact forward launch with HIP events on the
@@ -399,7 +475,7 @@ class NativeWorkload:
         against 8 TB/s. The first entry is the dominant kernel; the others ride along."""
         B = self.args.batch
         u = self.fd.unet.ucfg
-        T = self.tc + self.tp
+        T = u.frames
         out = []
         todo = list(self.layer_ids())
         while todo:
@@ -418,7 +494,8 @@ class NativeWorkload:
             if layer in self.CORE_SPLIT and launched.startswith('attn_core_kernel'):
                 # the unfused route: this entry is the core launch alone; its convs follow
                 what = what + ' — unfused route: the attention core launch alone'
-                todo[0:0] = [(i, 'mfma', None, w) for i, w in self.CORE_SPLIT[layer]]
+                shapes = {k: tuple(v.shape) for k, v in self.fd.unet.state_dict().items()}
+                todo[0:0] = [(i, 'mfma', None, layer_what(i, u, shapes)) for i, _ in self.CORE_SPLIT[layer]]
             arith = kernel_arith(kname, self.precision) if kname else ('fp32' if self.precision == 'fp32' else 'f16x3')
             traffic, src = self._traffic(layer, kname)
             if bound == 'mfma':
@@ -431,7 +508,8 @@ class NativeWorkload:
                     e['peak_note'] = (f'f16x3 qkv/proj + bf16 QK^T/PV: {frac_core:.3f} of the FLOPs at {BF16_PEAK_TFLOPS}, '
                                       f'the rest at {F16X3_PEAK_TFLOPS:.1f} TFLOP/s (FLOP-weighted harmonic peak)')
             else:
-                ch, hw, nt = self.HBM_BYTES[layer](u, T)
+                shapes = {k: tuple(v.shape) for k, v in self.fd.unet.state_dict().items()}
+                ch, hw, nt = self.HBM_BYTES[layer](u, T, shapes)
                 nbytes = 4 * B * nt * hw * ch
                 achieved = nbytes / (ms_layer * 1e-3) / 1e9
                 e = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -582,7 +660,12 @@ def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
         pairs = O.ddim_pairs(T_sched, steps_per_round) if ddim else None
         # a warm step + n_steps timed ones, all inside the sampler's step list
         n_steps = max(1, min(n_steps, (len(pairs) if ddim else T_sched) - 1))
-        runs = [(threads, B) for B in ([1, steady_batch] if steady_batch > 1 else [1])]
+        # B = 1, 2 and the steady batch: on the GPU box's host the oracle's per-clip cost is lowest at
+        # B = 2 and rises past it (B = 4: 3x the CPU-seconds of B = 2 for 2x the work, no cgroup
+        # throttling — a cache effect, profiles/r06_cpu_scaling.log); every point is reported and
+        # the value is the best of them
+        bs = sorted({1, min(2, steady_batch), steady_batch}) if steady_batch > 1 else [1]
+        runs = [(threads, B) for B in bs]
         if slice_threads < threads:
             runs.append((slice_threads, 1))
         points = []
@@ -615,9 +698,11 @@ def cpu_baseline(fd, rounds, steps_per_round, n_steps, w, steady_batch=4):
     return {'value': best['frames_per_s'], 'unit': 'frames/s', 'cores': cores, 'threads': threads,
             'kind': 'port', 'cpu_model': cpu_model(), 'batch_points': points,
             'visible_cores': visible, 'cgroup_cpus': cgroup_cpus(),
-            'baseline_method': 'r04: every host core the process may use (sched affinity capped by the cgroup '
-                               'CPU quota; value) + the OMP_NUM_THREADS slice at B=1 where smaller; median of '
-                               f'{n_steps} timed steps per point (r03: the OMP slice only, 3 steps)',
+            'baseline_method': 'r06: every host core the process may use (sched affinity capped by the cgroup '
+                               'CPU quota) at B = 1, 2 and the steady batch, value = the best per-clip point (the '
+                               'oracle\'s per-clip cost is lowest at B = 2 on this host and rises past it: a cache '
+                               'effect, not cgroup throttling, profiles/r06_cpu_scaling.log) + the OMP_NUM_THREADS '
+                               f'slice at B=1 where smaller; median of {n_steps} timed steps per point',
             'sample': f'oracle (PyTorch-CPU fp32) on {threads} threads = every usable host core ({visible} '
                       f'visible, cgroup quota {cgroup_cpus()}): encoder round '
                       f'({t_enc:.3f} s) and decode round ({t_dec:.3f} s) at B=1, {n_steps} '
@@ -671,7 +756,12 @@ def run_rank(args):
         if args.dump:
             torch.save(out.detach().cpu(), args.dump)
         meta = json.load(open(os.path.join(REPO, 'BASELINE.json')))
-        result = {'metric': meta['metric'], 'value': round(value, 4), 'unit': 'frames/s', 'n_gpus': world,
+        T_ = wl.fd.diffusion.num_timesteps if hasattr(wl, 'fd') else 0
+        sampler_ = f'DDPM {T_}' if args.sampling_steps >= T_ else f'DDIM {args.sampling_steps}'
+        label = meta['metric'] if args.stub else metric_label(
+            args.config, meta['metric'], sampler_, CONFIG_NAMES[args.config], wl.tc, args.total_pred,
+            wl.w['baseline'].split(':')[0])
+        result = {'metric': label, 'value': round(value, 4), 'unit': 'frames/s', 'n_gpus': world,
                   'steps': steps, 'warmup': args.warmup, 'ms_per_step': round(el / steps * 1e3, 4),
                   'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None}
         result.update(wl.describe())
