@@ -114,8 +114,10 @@ def kernel_peak(arith, core_frac=0.0):
 
 # BASELINE.json configs as bench workloads (tc / tp per round, rounds =
 # ceil(total_pred / tp); the sampler of the dataset's eval script). `batch` = clips per GPU:
-# the BASELINE batch split over its GPU count where it names one (KTH: 64 on 4 GPUs), else
-# what one MI355X runs in a few minutes. The BAIR line is the metric (configs[1]).
+# the BASELINE batch split over its GPU count where it names one (KTH: 64 on 4 GPUs), else the
+# batch past which the per-clip step cost stops falling (round 6, profiles/r06_batch_cfg.txt: ms per
+# clip-step Cityscapes 1.10 / 0.45 / 0.38 at 8 / 32 / 64, UCF 9.70 / 8.93 at 4 / 8, SMMNIST 0.519 /
+# 0.495 at 64 / 128). The BAIR line is the metric (configs[1]).
 WORKLOADS = {
     # BAIR: 128 clips per GPU (round 5 sweep, DDIM-20 generations on one box: 0.413 / 0.396 / 0.391 /
     # 0.397 ms per clip-step at B = 64 / 128 / 192 / 256 — the small levels' launches fill the chip
@@ -125,13 +127,13 @@ WORKLOADS = {
     'kth': dict(image=64, tc=10, tp=20, total_pred=40, sampling_steps=100, timesteps=1000, batch=16, occ=False,
                 precision=None, cpu_steady=2, baseline='configs[2]: KTH 64x64 ch1, cond=10 pred=40, DDIM 100 steps, batch=64 on 4 GPUs',
                 lead=(6, 'level-0 shifted STW attention (ada 4x4x4 windows, dim_head 16), fused LN/qkv/RoPE/softmax/PV/proj')),
-    'cityscapes': dict(image=128, tc=2, tp=5, total_pred=28, sampling_steps=1000, timesteps=1000, batch=8, occ=True,
+    'cityscapes': dict(image=128, tc=2, tp=5, total_pred=28, sampling_steps=1000, timesteps=1000, batch=64, occ=True,
                        precision=None, cpu_steady=2, baseline='configs[3]: Cityscapes 128x128 ch3, cond=2 pred=28, DDPM 1000 steps',
                        lead=(6, 'level-0 shifted STW attention (ada_u22 4x4x4 windows, dim_head 32), fused LN/qkv/RoPE/softmax/PV/proj')),
-    'ucf': dict(image=256, tc=4, tp=12, total_pred=12, sampling_steps=10, timesteps=1000, batch=4, occ=True,
+    'ucf': dict(image=256, tc=4, tp=12, total_pred=12, sampling_steps=10, timesteps=1000, batch=8, occ=True,
                 precision='bf16_attn', cpu_steady=1, cpu_steps_max=1, baseline='configs[4]: UCF-101 256x256 ch3, cond=4 pred=12, bf16 MFMA attention',
                 lead=(6, 'level-0 shifted STW attention (ada_u22 4x4x4 windows), fused, bf16 QK^T / PV')),
-    'smmnist': dict(image=64, tc=10, tp=10, total_pred=10, sampling_steps=100, timesteps=100, batch=64, occ=True,
+    'smmnist': dict(image=64, tc=10, tp=10, total_pred=10, sampling_steps=100, timesteps=100, batch=128, occ=True,
                     precision=None, baseline='configs[0]: SMMNIST 64x64 ch1, cond=10 pred=10, DDPM 100 steps',
                     lead=(6, 'level-0 shifted STW attention (C 64, 2x4x4 windows), fused LN/qkv/proj')),
 }
