@@ -90,7 +90,13 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tt = wave & 1;
   const int h = lane >> 5, lc = lane & 31;
-  const int gidx = blockIdx.x * (NW / 2) + (wave >> 1);  // the wave's window
+  // XCD-contiguous workgroup order (grid a multiple of 8, host): workgroup b runs on XCD b mod 8 and
+  // takes logical slot (b mod 8) G / 8 + b / 8, so the workgroups whose tiles share 128-B output
+  // lines (the two 16-column halves of a 32-column row) run on one XCD and their partial lines merge
+  // in its L2 instead of leaving it as two half-line write-backs
+  const int G8 = (int)gridDim.x;
+  const int bid = ((G8 & 7) || (dbg & 64)) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (G8 >> 3) + (blockIdx.x >> 3));
+  const int gidx = bid * (NW / 2) + (wave >> 1);  // the wave's window
   const bool active = gidx < total_groups;
   const int b = active ? gidx / groups_per_sample : 0;
   const int grp = active ? gidx % groups_per_sample : 0;
@@ -149,7 +155,7 @@ __global__ __launch_bounds__(NW * 64) void stw64_x3_kernel(float* x, long sb, lo
   const int mb_wave = __builtin_amdgcn_readfirstlane(pat * 8 * 4096 * 4);
   // TILE: the workgroup's first window (all its windows share (b, wd, wh)) and the lane's k-th
   // 8-B piece: LDS float offset, global byte offset (past the extent for a padded frame)
-  const int grp0 = TILE ? (blockIdx.x * WPG) % groups_per_sample : 0;
+  const int grp0 = TILE ? (bid * WPG) % groups_per_sample : 0;
   const int ww0 = grp0 % nWw, wh0 = (grp0 / nWw) % nWh, wd0 = grp0 / (nWw * nWh);
   // piece i of the lane: channel c0 + CPI i, the same (frame, row, column pair) for every i, so the
   // offsets are a base + i x a stride (32-bit: the host checks the sample's extent < 2^30 B)
@@ -529,9 +535,14 @@ void launch(hipStream_t s, const View& x, const AttnGeom& g, int groups, const f
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
   const int total = x.B * groups;
-  const int grid = (total + NW / 2 - 1) / (NW / 2);
+  // EXTDM_STW64_XCD=0: dispatch order (A/B); else the grid rounded up to a multiple of 8 for the
+  // XCD-contiguous order (the extra workgroups' windows lie past `total`: inactive)
+  static const bool xcd = [] { const char* v = getenv("EXTDM_STW64_XCD"); return !(v && v[0] == '0'); }();
+  int grid = (total + NW / 2 - 1) / (NW / 2);
+  if (xcd && grid >= 64) grid = (grid + 7) & ~7;
   note_kernel("stw64_x3_kernel<%d, %d, %d, %s, %s>", C, DH, NW, BF ? "true" : "false", tile ? "true" : "false");
-  static const int dbg = [] { const char* v = getenv("EXTDM_STW64_DBG"); return v ? atoi(v) : 0; }();
+  static const int dbg0 = [] { const char* v = getenv("EXTDM_STW64_DBG"); return v ? atoi(v) : 0; }();
+  const int dbg = dbg0 | (xcd && grid >= 64 ? 0 : 64);  // 64: dispatch order (no remap)
   auto kern = tile ? &stw64_x3_kernel<C, DH, NW, BF, TILE_OK> : &stw64_x3_kernel<C, DH, NW, BF, false>;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NW * 64), lds, s, x.p, x.sb, x.sc, x.st, g, gamma,
                      reinterpret_cast<const _Float16*>(wpk), wsc, bp, mbias, npat, rcos, rsin, q_scale, groups, total,
