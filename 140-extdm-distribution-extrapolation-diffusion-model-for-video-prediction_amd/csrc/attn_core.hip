@@ -24,6 +24,8 @@
 //   V^T is read from an LDS copy of V in that same key order.
 // Masks as the fp32 kernels (attn.hip): shifted-window region mismatch adds -100, padded
 // keys and (temporal) other pixels' frames are -inf.
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace extdm {
@@ -143,14 +145,17 @@ __global__ __launch_bounds__(256) void attn_core_kernel(const float* __restrict_
                                                         const float* __restrict__ bias_dense, int bstride,
                                                         const float* __restrict__ rcos,
                                                         const float* __restrict__ rsin, float q_scale,
-                                                        int* __restrict__ range_flag) {
+                                                        int* __restrict__ range_flag, int xcd) {
   constexpr int KST = DH / 16;  // k-steps of the QK^T contraction
   constexpr int RH = DH / 2;     // rotary pairs per head
   __shared__ float Vs[4][32 * NT][33];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = lane & 31, h = lane >> 5;
-  // a block = one token group, its waves walk the heads
-  const int gidx = blockIdx.x;
+  // a block = one token group, its waves walk the heads. xcd: XCD-contiguous group order (grid a
+  // multiple of 8): neighbouring windows, which read the same 128-B lines of qkv (a 4-wide window
+  // row is 16 B of each line), run on one XCD and share its L2
+  const int G8 = (int)gridDim.x;
+  const int gidx = xcd ? (int)((blockIdx.x & 7) * (G8 >> 3) + (blockIdx.x >> 3)) : (int)blockIdx.x;
   if (gidx >= total_groups) return;
   const int b = gidx / groups_per_sample, grp = gidx % groups_per_sample;
   const int per = g.D <= 16 ? 16 : 32;  // MODE 1: frame slots per pixel
@@ -314,12 +319,16 @@ bool attention_core(hipStream_t s, const View& qkv, const View& o, const AttnGeo
   }
   const int total = qkv.B * groups;
   int* flag = x3_range_ptr();
+  // EXTDM_CORE_XCD=0: dispatch order (A/B)
+  static const bool xcd_on = [] { const char* v = getenv("EXTDM_CORE_XCD"); return !(v && v[0] == '0'); }();
+  const int xcd = xcd_on && total >= 64 ? 1 : 0;
+  const int grid = xcd ? (total + 7) & ~7 : total;
 #define CORE_GO(M, X, NT_, DH_)                                                                              \
   do {                                                                                                       \
   note_kernel("attn_core_kernel<%d, %s, %d, %d>", M, X ? "true" : "false", NT_, DH_);                         \
-  hipLaunchKernelGGL((attn_core_kernel<M, X, NT_, DH_>), dim3(total), dim3(256), 0, s, qkv.p, qkv.sb, qkv.sc,     \
+  hipLaunchKernelGGL((attn_core_kernel<M, X, NT_, DH_>), dim3(grid), dim3(256), 0, s, qkv.p, qkv.sb, qkv.sc,      \
                      qkv.st, o.p, o.sb, o.sc, g, heads, groups, total, bias_dense, bstride, rope_cos, rope_sin,    \
-                     q_scale, flag);                                                                          \
+                     q_scale, flag, xcd);                                                                     \
   } while (0)
   if (dim_head == 16) {
     if (nt == 2) CORE_GO(0, true, 2, 16);
