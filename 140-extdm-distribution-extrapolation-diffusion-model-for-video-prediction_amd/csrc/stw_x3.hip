@@ -247,13 +247,19 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   const int t1pw = (32 / PER) * wave + lc / PER;
   const int t1idx = (t1pw >> 2) * (4 * PER) + (lc % PER) * 4 + (t1pw & 3);
   int trow[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // element offset of tile row r in a channel plane
+  // rows of a padded frame (D odd, Dp = D + 1: frame D of the padded volume): loaded from frame D - 1
+  // (any finite data: those tokens normalise to 0 like the reference's zero padding), never stored
+  int rowpad = 0;
   if (T0) {
     const int grp0 = (wg * NW) % groups_per_sample;
     const int nWw = g.Wp / g.ws2, nWh = g.Hp / g.ws1;
     const int wh = (grp0 / nWw) % nWh, wd = grp0 / (nWw * nWh);
 #pragma unroll
-    for (int r = 0; r < 8; ++r)
-      trow[r] = ((wd * 2 + (r >> 2) + g.ss0) % g.Dp) * (int)st + ((wh * 4 + (r & 3) + g.ss1) % g.Hp) * 32;
+    for (int r = 0; r < 8; ++r) {
+      const int fd = (wd * 2 + (r >> 2) + g.ss0) % g.Dp;
+      rowpad |= (fd >= g.D ? 1 : 0) << r;
+      trow[r] = (fd < g.D ? fd : g.D - 1) * (int)st + ((wh * 4 + (r & 3) + g.ss1) % g.Hp) * 32;
+    }
     const int r = lane >> 3, q = (lane & 7) ^ r;
     int roff = trow[0];
 #pragma unroll
@@ -296,8 +302,8 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 
   // ---- 1. normalisation into register fragments ----
   Tok me;
-  if (T0) {  // every token of a tile window exists and lies inside the volume
-    me.pos = 0; me.valid = 1; me.exists = 1; me.lab = 0; me.rpos = lc;
+  if (T0) {  // every token of a tile window exists; rows of a padded frame are not valid
+    me.pos = 0; me.valid = ((rowpad >> (lc >> 2)) & 1) ? 0 : 1; me.exists = 1; me.lab = 0; me.rpos = lc;
   } else {
     me = token_of<MODE>(lc, g, st, grp);
   }
@@ -822,7 +828,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 #pragma unroll
       for (int i = 1; i < 8; ++i) roff = r == i ? trow[i] : roff;
       const float4 v = *reinterpret_cast<const float4*>(tileT + c * 256 + r * 32 + qs * 4);
-      *reinterpret_cast<float4*>(ob + (long)c * osc + roff + 4 * (qs ^ r)) = v;
+      if (!((rowpad >> r) & 1)) *reinterpret_cast<float4*>(ob + (long)c * osc + roff + 4 * (qs ^ r)) = v;
     }
   }
 }
@@ -846,7 +852,7 @@ bool attn_x3_tile1_ok(const View& x, const View& out, const AttnGeom& g, int gro
 bool attn_x3_tile_ok(const View& x, const View& out, const AttnGeom& g, int groups) {
   static const bool off = [] { const char* v = getenv("EXTDM_X3_NO_TILE"); return v && v[0] && v[0] != '0'; }();
   return !off && g.mode == 0 && g.ws0 == 2 && g.ws1 == 4 && g.ws2 == 4 && g.W == 32 && g.Wp == 32 && g.H == g.Hp &&
-         g.D == g.Dp && groups % 8 == 0 && x.p == out.p && x.sc == out.sc && x.sb == out.sb && x.st == out.st &&
+         g.D >= 1 && g.Dp <= g.D + 1 && groups % 8 == 0 && x.p == out.p && x.sc == out.sc && x.sb == out.sb && x.st == out.st &&
          x.st == (long)x.H * x.W && x.sc % 4 == 0 && x.sb % 4 == 0 && ((uintptr_t)x.p & 15) == 0;
 }
 
@@ -885,6 +891,11 @@ void launch_nw(hipStream_t s, const View& x, const View& out, const AttnGeom& g,
     (void)hipMemsetAsync(ts, 0, (size_t)total * 24 * sizeof(long long), s);
   }
   constexpr bool TILE_OK = C == 64 && NW == 8;
+  // EXTDM_X3_TILE_DBG=1 (diagnostic): the route's geometry per launch to stderr
+  static const bool tdbg = getenv("EXTDM_X3_TILE_DBG") != nullptr;
+  if (tdbg)
+    fprintf(stderr, "attn_x3 MODE %d C %d tile %d: D %d Dp %d H %d Hp %d W %d Wp %d ws %d %d %d groups %d sc %ld sb %ld st %ld p %p\n",
+            MODE, C, (int)tile, g.D, g.Dp, g.H, g.Hp, g.W, g.Wp, g.ws0, g.ws1, g.ws2, groups, x.sc, x.sb, x.st, (void*)x.p);
   auto kern = tile ? &attn_x3_kernel<C, MODE, DH, NW, TILE_OK, BF> : &attn_x3_kernel<C, MODE, DH, NW, false, BF>;
   note_kernel("attn_x3_kernel<%d, %d, %d, %d, %s, %s>", C, MODE, DH, NW, tile && TILE_OK ? "true" : "false",
               BF ? "true" : "false");

@@ -12,14 +12,26 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 
 pkg = importlib.import_module(bench.PKG)
-LATENT = {'bair': (32, 16), 'kth': (32, 16), 'smmnist': (64, 64), 'cityscapes': (32, 32), 'ucf': (128, 64)}
+
+
+def unet_config(cfg_name):
+    """The UnetConfig bench.py's FlowDiffusion builds for the workload (round 6: read from the
+    model itself — the hard-coded latent / fea_size table had SMMNIST at 64 / 64 and Cityscapes'
+    fea_size at 32, not the bench's 32 / 32 and 16)."""
+    a = bench.parse(['--config', cfg_name])
+    w = bench.WORKLOADS[cfg_name]
+    wrapper, arch = pkg.configs.dm_arch(cfg_name)
+    cfg = pkg.configs.dm_config(cfg_name, pred_frames=a.tp, sampling_timesteps=a.sampling_steps,
+                                estimate_occlusion_map=w['occ'])
+    cfg['dataset_params']['frame_shape'] = w['image']
+    fd = pkg.FlowDiffusion(config=cfg, is_train=False, Unet3D_architecture=arch, wrapper=wrapper,
+                           timesteps=w['timesteps'])
+    return fd.unet.ucfg
 
 
 def make(cfg_name):
     w = bench.WORKLOADS[cfg_name]
-    _, arch = pkg.configs.dm_arch(cfg_name)
-    lat, fs = LATENT[cfg_name]
-    ucfg = pkg.spec.UnetConfig.for_arch(arch, tc=w['tc'], tp=w['tp'], latent=lat, fea_size=fs)
+    ucfg = unet_config(cfg_name)
     prec = os.environ.get('PREC') or w['precision'] or pkg._lib.DEFAULT_PRECISION
     B = int(os.environ.get('B', w['batch']))
     torch.cuda.set_device(0)

@@ -109,6 +109,43 @@ def test_attention_core_heads6_vs_oracle(prefix, level, shifted):
     parity_log.check(err, ATT_BAR)
 
 
+@pytest.mark.parametrize('prefix,shifted', [('downs.0.1', True), ('downs.0.3', False)])
+def test_window32_tile_odd_frames_vs_oracle(prefix, shifted):
+    """SMMNIST's wo_ref denoiser at its own shapes: 2x4x4 windows over 9 + 10 = 19 frames, padded to
+    20, so the last window row holds a padded frame. Round 6: the fused kernel's LDS tile path
+    (attn_x3_kernel TILE) covers it (rows of the padded frame loaded from frame D - 1, normalised to
+    0 like the reference's zero padding, never stored); before, an odd frame count fell back to
+    per-lane 4-B loads and stores."""
+    import dataclasses
+    from oracle import extdm_oracle as O
+    cfg = dataclasses.replace(CONFIGS['woref_smmnist'], tp=10)  # the SMMNIST bench: 10 -> 10
+    key = ('woref_t19', 'f16x3')
+    if key not in _H:
+        h = pkg._lib.Handle(cfg, 1000, 2, 0, precision='f16x3')
+        sd = make_sd(cfg)
+        sd.update(pkg.schedule_buffers(1000))
+        h.load_state(sd)
+        h.finalize()
+        _H[key] = (h, sd)
+    h, sd = _H[key]
+    assert cfg.frames == 19 and cfg.latent == 32
+    gen = torch.Generator().manual_seed(41)
+    x = torch.randn(2, cfg.dim, cfg.frames, cfg.latent, cfg.latent, generator=gen) * 1.5 + 0.3
+    out = torch.empty(x.shape, device=DEV)
+    h.attn_layer(prefix, x.to(DEV), out, shifted=shifted)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        win = tuple(cfg.window)
+        ref = O.stw_attention(sd, prefix, x, win, tuple(w // 2 for w in win) if shifted else (0, 0, 0),
+                              cfg.heads, cfg.dim_head)
+    err = (out.cpu() - ref).abs().max().item()
+    out2 = torch.empty(x.shape, device=DEV)
+    h.attn_layer(prefix, x.to(DEV), out2, shifted=shifted)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), out2.cpu())
+    parity_log.check(err, ATT_BAR, f'wo_ref {cfg.frames} frames')
+
+
 # 64-token windows (ada / ada_u22 4x4x4): the fused stw64_x3 route. ada_kth: dim_head 16 (two
 # heads per 32-row unit), T = 30 -> padded to 32 frames; u22_city: dim_head 32, T = 7 -> 8
 # (a padded frame inside every window of the last window row). `level`: the latent halvings
