@@ -286,7 +286,10 @@ struct AttnGeom {
   int ws0, ws1, ws2; // effective window
   int ss0, ss1, ss2; // effective shift
   int Dp, Hp, Wp;    // padded extents
+  int per;           // mode 1, fused kernels (stw_x3.hip): frame slots per pixel (8, 16, 32; 0 = 16 / 32 by D)
 };
+// frame slots per pixel of the fused temporal attention (32 tokens per wave = 32 / per pixels)
+__host__ __device__ inline int temporal_slots(const AttnGeom& g) { return g.per ? g.per : (g.D <= 16 ? 16 : 32); }
 // Attention core (attn_core.hip): QK^T / softmax / PV over qkv [B][3*heads*32][T][H][W]
 // into o [B][heads*32][T][H][W], token groups of <= 64 (temporal: <= 32 frames),
 // dim_head 32; f16x3 (fp32-faithful) or bf16 (EXTDM_PRECISION_BF16_ATTN). False if the

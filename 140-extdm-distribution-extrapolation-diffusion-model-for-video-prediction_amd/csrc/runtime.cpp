@@ -948,10 +948,11 @@ struct ExtdmHandle {
   // temporal attention (one table): T5 bias of (query frame, key frame), -inf for another
   // pixel's frames and for key frames >= D (32-token groups of 32 / per pixels)
   const float* temporal_mask_bias(const AttnGeom& g, float s2) {
-    const std::string key = "temporal|" + std::to_string(g.D) + "|" + std::to_string(std::ilogb(s2));
+    const int per = temporal_slots(g);
+    const std::string key = "temporal|" + std::to_string(g.D) + "|" + std::to_string(per) + "|" + std::to_string(std::ilogb(s2));
     auto it = mask_bias.find(key);
     if (it != mask_bias.end()) return it->second.first;
-    const int nh = cfg.heads, per = g.D <= 16 ? 16 : 32;
+    const int nh = cfg.heads;
     REQUIRE(nh == 8 && g.D <= 32, "temporal bias + mask table: shape");
     std::vector<float> t((size_t)nh * 1024, 0.f);
     for (int hd = 0; hd < nh; ++hd)
@@ -1232,6 +1233,10 @@ struct ExtdmHandle {
     const int T = x.T;
     AttnGeom g{};
     g.mode = 1; g.D = T; g.H = x.H; g.W = x.W;
+    // fused kernels: 8 frame slots per pixel (four pixels per wave) for D <= 8 (Cityscapes' 7
+    // frames filled 14 of a wave's 32 tokens at 16 slots); EXTDM_X3_PER8=0: 16 / 32 only (A/B)
+    static const bool per8 = [] { const char* v = getenv("EXTDM_X3_PER8"); return !(v && v[0] == '0'); }();
+    g.per = T <= 8 && per8 ? 8 : (T <= 16 ? 16 : 32);
     const bool fused_x3 = x3_attn_ok(x.C, T, 1) && out.sc == x.sc && out.st == x.st;
     if (core_attn(T, 32, fused_x3, false)) {
       // double-LN prologue, f16x3 qkv conv, the core (bf16 or f16x3 MFMA), f16x3 to_out + residual

@@ -69,7 +69,7 @@ __device__ __forceinline__ Tok token_of(int tk, const AttnGeom& g, long st, int 
     o.rpos = tk;
   } else {
     const int HW = g.H * g.W;
-    const int per = g.D <= 16 ? 16 : 32;
+    const int per = temporal_slots(g);
     const int p = tk / per, t = tk % per;
     const int hw = grp * (32 / per) + p;
     o.exists = t < g.D && hw < HW;
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   float* const tileT = reinterpret_cast<float*>(wsm + 2 * UL::HALVES);
   // behind the tile: T0 gamma + proj bias, T1 gamma + LayerNorm w + b (192 floats)
   float* const parL = tileT + C * 256;
-  const int PER = g.D <= 16 ? 16 : 32;                                     // T1: frame slots per pixel
+  const int PER = temporal_slots(g);                                       // T1: frame slots per pixel
   const int hw0 = T1 ? ((wg * NW) % groups_per_sample) * (32 / PER) : 0;  // T1: the workgroup's first pixel
   if (T1) {
     const int lt = lane % PER, lq = lane / PER;
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
   // 16 frame planes per instruction, 8 bytes each, and every 64-B line is written by 8
   // waves. Instead the workgroup's 16 consecutive pixels x D frames x C channels go through
   // LDS ([c][t][16 px], rows padded for conflict-free lane writes) and leave as 64-B rows.
-  const bool lds_epi = !T1 && MODE == 1 && C == 64 && NW == 8 && g.D <= 16 && groups_per_sample % NW == 0 &&
+  const bool lds_epi = !T1 && MODE == 1 && C == 64 && NW == 8 && temporal_slots(g) == 16 && groups_per_sample % NW == 0 &&
                        (g.H * g.W) % 16 == 0 && (osc & 3) == 0 && (st & 3) == 0 && (((uintptr_t)out) & 15) == 0;
   if (T1) {
     // residual from the tile, the result back into it (each (channel, frame, pixel) is one
@@ -839,7 +839,7 @@ __global__ __launch_bounds__(NW * 64) void attn_x3_kernel(const float* x, float*
 bool attn_x3_tile1_ok(const View& x, const View& out, const AttnGeom& g, int groups) {
   static const bool off = [] { const char* v = getenv("EXTDM_X3_NO_TILE"); return v && v[0] && v[0] != '0'; }();
   static const bool only16 = [] { const char* v = getenv("EXTDM_X3_TILE1_16"); return v && v[0] && v[0] != '0'; }();
-  const int per = g.D <= 16 ? 16 : 32;
+  const int per = temporal_slots(g);
   return !off && g.mode == 1 && g.D >= 1 && g.D <= 32 && (!only16 || g.D == 16) && (g.H * g.W) % (256 / per) == 0 &&
          groups % 8 == 0 && x.st == (long)x.H * x.W &&
          x.st % 4 == 0 && x.sc % 4 == 0 && x.sb % 4 == 0 && out.sc % 4 == 0 && out.sb % 4 == 0 && out.st == x.st &&
@@ -1000,7 +1000,7 @@ bool temporal_x3(hipStream_t s, const View& x, const View& out, const AttnGeom& 
   const int npat = 1;
   if (!attn_x3_supported(x.C, g.D, dim_head, heads) || g.D > 32 || !extent_ok(x, g) || !extent_ok(out, g)) return false;
   if (out.sc != x.sc || out.st != x.st) return false;
-  const int ppb = g.D <= 16 ? 2 : 1;
+  const int ppb = 32 / temporal_slots(g);
   const int groups = (g.H * g.W + ppb - 1) / ppb;
   if (dim_head == 32)
     return dispatch_c<1, 32>(s, x, out, g, groups, gamma, ln_w, ln_b, wpk, wsc, nullptr, mbias, npat, rcos,

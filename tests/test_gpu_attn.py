@@ -211,8 +211,8 @@ def test_window64_attention_bf16_vs_oracle(name, prefix, level, shifted):
 
 
 # temporal attention at the other configs' frame counts: KTH 30 (dim_head 16), wo_ref 14 (the golden
-# config's tc - 1 + tp), Cityscapes 7 — the LDS tile path with 32 / 16 frame slots per pixel and the slots
-# past D masked (stw_x3.hip T1, round 5)
+# config's tc - 1 + tp), Cityscapes 7 — the LDS tile path with 32 / 16 / 8 frame slots per pixel (one, two
+# or four pixels per wave; 8 since round 6) and the slots past D masked (stw_x3.hip T1)
 TEMPORAL = [('ada_kth', 'init_temporal_attn'), ('woref_smmnist', 'init_temporal_attn'),
             ('u22_city', 'init_temporal_attn')]
 
