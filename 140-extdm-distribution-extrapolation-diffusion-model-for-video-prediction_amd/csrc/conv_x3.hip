@@ -1133,21 +1133,23 @@ bool x3_mfast(const X3Args& a, const X3Tile& tl, unsigned ntiles) {
 }
 
 // 1x1 256-row convs on 256 x 256 tiles (twice the MFMAs per staged weight fragment) when that
-// tiling still fills >= 3/4 of the CUs in one round at the reference batch 64 -- a function of
-// the per-sample geometry only, like split_slices, so a clip's tiling never depends on its
-// shard (both tilings sum K in the same order: bitwise equal). The level-2 Tmodulator 460 ->
-// 353 us at B = 64; the level-3 / mid ones (56 workgroups at 256 px) keep 256 x 128 + split-K.
-// EXTDM_X3_BN1=128 keeps 256 x 128 everywhere (A/B).
+// tiling still fills >= 3/4 of the CUs in one round at this launch's batch (round 6; it was the
+// reference batch 64, which left KTH's 16-clip Tmodulator 7680 -> 5120 on 80 workgroups). Both
+// tilings sum K in the same order, so the choice may depend on the batch: a clip's result is
+// bitwise the same either way (tests/test_gpu_parity.py batch-slice test). The level-2 Tmodulator
+// 460 -> 353 us at B = 64; the level-3 / mid ones (56 workgroups at 256 px) keep 256 x 128 + split-K.
+// EXTDM_X3_BN1=128 keeps 256 x 128 everywhere, EXTDM_X3_BN1=64 restores the batch-64 rule (A/B).
 bool x3_bn256(const View& out, const PackedW& w, const ConvEpi& epi) {
   static const int bn1 = [] { const char* v = getenv("EXTDM_X3_BN1"); return v ? atoi(v) : 256; }();
-  if (bn1 != 256 || w.KH != 1 || w.xbm != 256 || w.xbn != 128 || epi.res_aff) return false;
+  if ((bn1 != 256 && bn1 != 64) || w.KH != 1 || w.xbm != 256 || w.xbn != 128 || epi.res_aff) return false;
   const int H = out.H, W = out.W;
   if (W > 256 || 256 % W != 0) return false;
   const int TH = std::min(H, 256 / W);
   if (256 % (TH * W) != 0) return false;
   const long NP = 256 / (TH * W), nrow = (H + TH - 1) / TH;
-  const long nwg64 = (64L * out.T + NP - 1) / NP * nrow * ((out.C + 255) / 256);
-  return nwg64 >= 192;
+  const long Bref = bn1 == 64 ? 64L : (long)out.B;
+  const long nwg = (Bref * out.T + NP - 1) / NP * nrow * ((out.C + 255) / 256);
+  return nwg >= 192;
 }
 
 bool conv_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w0,

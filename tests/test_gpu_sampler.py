@@ -148,3 +148,20 @@ def test_sampler_bitwise_stable_beside_a_second_gpu_process(tmp_path):
     for r in res:
         assert r['repeats'] > 10, r
         assert r['mismatches'] == 0, r
+
+
+def test_unet_batch_slice_bitwise():
+    """The full BAIR denoiser at B = 64 and the first 8 of those clips alone: eps bitwise equal. The
+    tile choices that depend on the launch's batch (the 1x1 256 x 256 vs 256 x 128 tiles, round 6)
+    must not change a clip's result, or shards of a batch would differ from the unsharded run."""
+    cfg_b = CONFIGS["bair"]
+    h = handle(64)
+    x, t, cond, fea = unet_inputs(cfg_b, B=64, seed=19)
+    tt = torch.full((64,), 617, dtype=torch.long)
+    eps = torch.empty(x.shape, device=DEV)
+    h.unet_forward(x.to(DEV), tt.to(DEV), cond.to(DEV), fea.to(DEV), eps)
+    eps8 = torch.empty((8,) + tuple(x.shape[1:]), device=DEV)
+    h.unet_forward(x[:8].contiguous().to(DEV), tt[:8].contiguous().to(DEV), cond[:8].contiguous().to(DEV),
+                   fea[:8].contiguous().to(DEV), eps8)
+    torch.cuda.synchronize()
+    assert torch.equal(eps[:8].cpu(), eps8.cpu())
