@@ -15,7 +15,7 @@ CSRC = os.path.join(HERE, 'csrc')
 REPO = os.path.dirname(HERE)
 INCLUDE = os.path.join(REPO, 'include')
 LIB = os.path.join(HERE, 'libextdm_hip.so')
-SOURCES = ['conv.hip', 'conv_halo.hip', 'conv_x3.hip', 'pw_x3.hip', 'conv_gemm_x3.hip', 'norm.hip', 'attn.hip', 'attn_core.hip', 'stw_fused.hip',
+SOURCES = ['conv.hip', 'conv_halo.hip', 'conv_x3.hip', 'pw_x3.hip', 'conv_gemm_x3.hip', 'conv_narrow.hip', 'norm.hip', 'attn.hip', 'attn_core.hip', 'stw_fused.hip',
            'stw_x3.hip', 'stw64_x3.hip', 'cross_x3.hip', 'xpath_x3.hip', 'fea_x3.hip', 'metrics.hip', 'sampler.hip', 'decoder.hip', 'lfae.hip', 'runtime.cpp']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['--offload-arch=gfx950', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', '-I', INCLUDE, '-I', CSRC]
@@ -37,7 +37,9 @@ PER_FILE = {'stw_x3.hip': ['-fno-slp-vectorize'] + VGPR_MFMA, 'stw64_x3.hip': ['
             # around the IEEE divisions) returned wrong values in 16-lane groups of one
             # component in ~9 % of launches while a second process ran on the GPU; scalar
             # fp32: 0 in 175 000 (tests/test_gpu_sampler.py)
-            'sampler.hip': ['-fno-slp-vectorize']}
+            'sampler.hip': ['-fno-slp-vectorize'],
+            # scalar v_fma_f32 chains (SLP paired them into v_pk_fma_f32 with lane shuffles)
+            'conv_narrow.hip': ['-fno-slp-vectorize']}
 OPT = {}
 
 

@@ -240,6 +240,7 @@ int conv_forward(hipStream_t s, const View& out, const View& in0, const View* in
   if (w.mode == MODE_CONV && stride == 1 && w.KH == 1 && w.KW == 1 && pad == 0 && !in1 &&
       pw_x3_forward(s, out, in0, w, epi_in))
     return 0;
+  if (w.wv && conv_narrow_forward(s, out, in0, in1, w, stride, pad, epi_in)) return 0;
   if (w.mode == MODE_CONV && stride == 1 && w.KH == w.KW && pad == w.KH / 2 &&
       conv_x3_forward(s, out, in0, in1, w, epi_in, &slots))
     return slots;

@@ -151,6 +151,10 @@ struct PackedW {
   void* gx = nullptr;
   float* gscale = nullptr;
   int gbm = 0, gnkt = 0;
+  // fp32 direct VALU layout [group][ci][ky * KW + kx][vcot rounded up to 4] (conv_narrow.hip), zero past M:
+  // KS x KS convs with few output channels
+  float* wv = nullptr;
+  int vcot = 0;
 };
 
 // Output-channel tile of the conv GEMM for M output channels (Mpad is a multiple of it).
@@ -377,6 +381,11 @@ bool noise_pool_x3_forward(hipStream_t s, const View& out, const View& x, const 
 // weights packed like noise_pool's (Pconv7c3); L a multiple of 32, Cout a multiple of 64
 bool conv7c3_x3_forward(hipStream_t s, const View& out, const View& x, const void* w, const float* rscale,
                         const float* bias, const View* add);
+// Few-output-channel KS x KS convs on fp32 VALU FMAs (conv_narrow.hip): narrow_cot(KS, M) is the
+// packer's output-channel group (0: not taken); false if the conv is not covered.
+int narrow_cot(int KS, int M);
+bool conv_narrow_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
+                         int stride, int pad, const ConvEpi& epi);
 bool conv_gemm_x3_forward(hipStream_t s, const View& out, const View& in0, const View* in1, const PackedW& w,
                           int stride, int pad, const ConvEpi& epi);
 void cross_attention(hipStream_t s, const float* q, const float* k, const float* v, float* o, int B, int C,
@@ -399,6 +408,9 @@ void bilinear_frames(hipStream_t s, const View& dst, const View& a, const View& 
 // per (b,c) mean and unbiased std (+eps) over T*H*W (u12:670-678)
 void adaptor_stats(hipStream_t s, const View& x, float* mean, float* std_, double* partials);
 void adaptor_normalize(hipStream_t s, const View& dst, const View& src, const float* mean, const float* std_);
+// zero frames 0 and T - 1 of every clip of a frame-major buffer (one launch; a 2-D memset of the
+// same rows ran at ~0.2 TB/s)
+void zero_pad_frames(hipStream_t s, const View& x);
 
 // Sampler step kernels.
 struct StepCoef {  // per sampler step (host-computed in fp32 exactly like the reference)

@@ -790,6 +790,16 @@ __global__ __launch_bounds__(256) void adaptor_norm_kernel(float* d, long dsb, l
   d[off5(dsb, dsc, dst_, b, c, t, hw)] = (s[off5(ssb, ssc, sst, b, c, t, hw)] - mean[bc]) / std_[bc];
 }
 
+// zero the first and last frame of every clip of a frame-major buffer (the 3x3x3 extrapolator's
+// temporal zero padding): grid.y = 2 B rows of `len` floats, float4 stores
+__global__ __launch_bounds__(256) void zero_pad_frames_kernel(float* p, long sb, long last, long len4) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= len4) return;
+  const int r = blockIdx.y;
+  float4* row = reinterpret_cast<float4*>(p + (long)(r >> 1) * sb + (r & 1) * last);
+  row[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 inline unsigned nblk(long n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
@@ -972,6 +982,15 @@ void adaptor_normalize(hipStream_t s, const View& d, const View& src, const floa
                        d.p + (long)b0 * d.sb, d.sb, d.sc, d.st, src.p + (long)b0 * src.sb, src.sb, src.sc, src.st,
                        d.C, d.T, d.HW(), mean + (long)b0 * d.C, std_ + (long)b0 * d.C);
   }
+}
+
+void zero_pad_frames(hipStream_t s, const View& x) {
+  // frame-major: frame t of clip b is st contiguous floats at b * sb + t * st
+  if (!(x.st == (long)x.C * x.HW() && x.sc == x.HW() && x.st % 4 == 0 && x.sb % 4 == 0 &&
+        ((uintptr_t)x.p & 15) == 0 && x.B <= 32767 && x.T >= 2))
+    throw std::invalid_argument("zero_pad_frames: needs a frame-major buffer of 16-byte aligned frames");
+  hipLaunchKernelGGL(zero_pad_frames_kernel, dim3(nblk(x.st / 4), 2 * x.B), dim3(256), 0, s, x.p, x.sb,
+                     (long)(x.T - 1) * x.st, x.st / 4);
 }
 
 }  // namespace extdm

@@ -183,7 +183,22 @@ struct ExtdmHandle {
         ci >= 16)
       pack_x3(pw, t.f, ci);
     if (x3_convs()) pack_gemm_x3(pw, a, 1);
+    if (kh == kw && narrow_cot(kh, co) > 0) pack_narrow(pw, t.f, ci);
     return packed[n] = pw;
+  }
+  // fp32 direct VALU layout (conv_narrow.hip): [group][ci][tap][vcot rounded up to 4], m =
+  // group * vcot + o
+  void pack_narrow(PackedW& pw, const std::vector<float>& w, int ci) {
+    const int kk = pw.KH * pw.KW, co = pw.M, cot = narrow_cot(pw.KH, co), ng = (co + cot - 1) / cot;
+    const int cotp = (cot + 3) & ~3;
+    std::vector<float> a((size_t)ng * ci * kk * cotp, 0.f);
+    for (int m = 0; m < co; ++m)
+      for (int c = 0; c < ci; ++c)
+        for (int tap = 0; tap < kk; ++tap)
+          a[(((size_t)(m / cot) * ci + c) * kk + tap) * cotp + m % cot] = w[((size_t)m * ci + c) * kk + tap];
+    pw.wv = dmalloc(a.size() * sizeof(float));
+    HIPCHK(hipMemcpy(pw.wv, a.data(), a.size() * sizeof(float), hipMemcpyHostToDevice));
+    pw.vcot = cot;
   }
   // f16x3 implicit-GEMM layout (conv_gemm_x3.hip) from the fp32 GEMM packing a
   // [npar][Kpad][Mpad]: [par][mtile][ktile][step][m32][hi|lo][lane][8], row m = mtile*BM +
@@ -1328,8 +1343,7 @@ struct ExtdmHandle {
         View hp = alloc_tm(B, C, nl + 2, Hh, Ww);
         View hn = hp.frames(1, nl);
         if (!plan) {
-          HIPCHK(hipMemset2DAsync(hp.p, hp.sb * 4, 0, hp.st * 4, B, s));
-          HIPCHK(hipMemset2DAsync(hp.p + (size_t)(nl + 1) * hp.st, hp.sb * 4, 0, hp.st * 4, B, s));
+          zero_pad_frames(s, hp);
           adaptor_normalize(s, hn, cur, mean, sd);
         }
         View win = hp;
