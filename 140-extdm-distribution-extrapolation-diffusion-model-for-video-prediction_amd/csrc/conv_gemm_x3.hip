@@ -10,6 +10,7 @@
 // fragments, rows pre-scaled by powers of two, undone by gscale[m] in the epilogue);
 // B is split into hi / lo while staging, as [hi|lo][step][n][16 k] with the 16-B halves
 // of a row swapped on bit 3 of n (conflict-free ds_read_b128 over 16 lanes).
+#include <algorithm>
 #include <cstdlib>
 
 #include "kernels.h"
@@ -37,6 +38,7 @@ struct GArgs {
   long N;
   int* range;
   int in_bytes;  // FAST: byte extent of in0 (the buffer descriptor's range; < 2^30)
+  const _Float16* wt; int nkt_t;  // TAPK: the tap-major packing (nullptr: none)
 };
 
 __device__ __forceinline__ float act_apply(float v, int act) {
@@ -55,7 +57,13 @@ __device__ __forceinline__ float act_apply(float v, int act) {
 // element's in-image test and its byte offset are computed once, and each load is a buffer
 // load with that offset (an invalid tap's offset lies past the extent: the load returns 0)
 // and the tile's channel offset in soffset: no per-element address math or branch.
-template <int KH, int KW, int BM, int MODE, bool FAST = false>
+// TAPK (tap-major K, k = tap * Cin + ci; Cin and the first source's channels multiples of 8,
+// 32-bit byte offsets; the host checks): a thread's 8-element gather group is 8 channels of
+// one tap of one source, so the tap, its in-image test and the pixel's byte offset are
+// computed once per group, the channel planes are wave-uniform bases (saddr loads), and the
+// nearest-x2 up convs gather the same way. For the 3x3 / 7x7 / up convs the ci-major order
+// leaves to the per-element path (32 % KH * KW != 0).
+template <int KH, int KW, int BM, int MODE, bool FAST = false, bool TAPK = false>
 __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
   constexpr int WAVES_M = BM >= 64 ? 2 : 1;
   constexpr int WAVES_N = 4 / WAVES_M;
@@ -86,7 +94,7 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
   const int mt = blockIdx.y;
   const int par = blockIdx.z;  // deconv parity (py, px)
   const int py = par >> 1, px = par & 1;
-  const _Float16* wbase = a.w + ((long)par * gridDim.y + mt) * a.nkt * AH;
+  const _Float16* wbase = a.w + ((long)par * gridDim.y + mt) * a.nkt * AH;  // a.w / a.nkt: the launch's packing
 
   // ---- per-thread gather column (B operand): column col, k groups kg and kg + 2 ----
   const int col = tid & (BN - 1);
@@ -139,6 +147,34 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
   }
 
   auto load_tile = [&](int kt) __attribute__((always_inline)) {
+    if (TAPK) {
+#pragma unroll
+      for (int g2 = 0; g2 < 2; ++g2) {
+        const int kb = __builtin_amdgcn_readfirstlane(kt * BK + 8 * (kg + 2 * g2));
+        const int tap = kb / a.Cin, ci0 = kb - tap * a.Cin;
+        const int ky = tap / KW, kx = tap - ky * KW;
+        const int iy = iy0 + ky, ix = ix0 + kx;
+        const bool ok = nvalid && tap < KK && iy >= 0 && iy < Hv && ix >= 0 && ix < Wv;
+        const int sy = MODE == MODE_UP2 ? (iy >> 1) : iy;
+        const int sx = MODE == MODE_UP2 ? (ix >> 1) : ix;
+        const bool s1 = ci0 >= a.C0;  // wave-uniform
+        const unsigned vo = ok ? (unsigned)(((s1 ? base1 : base0) + (long)sy * a.Win + sx) * 4) : 0u;
+        const float* plane = s1 ? a.in1 + (long)(ci0 - a.C0) * a.i1c : a.in0 + (long)(ci0 < a.Cin ? ci0 : 0) * a.i0c;
+        const int cst4 = (int)((s1 ? a.i1c : a.i0c) * 4);
+        // the group's first channel plane as the (uniform) buffer base: pixel offset in
+        // voffset, channel e's plane offset in soffset
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(plane), 0, -1, 0x00020000);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)vo, e * cst4, 0));
+          breg[g2][e] = ok ? v : 0.f;
+        }
+      }
+      const u32x4* ap = reinterpret_cast<const u32x4*>(wbase + (long)kt * AH);
+#pragma unroll
+      for (int p = 0; p < APASS; ++p) areg[p] = ap[p * 256 + tid];
+      return;
+    }
     if (FAST) {
 #pragma unroll
       for (int g2 = 0; g2 < 2; ++g2)
@@ -288,17 +324,32 @@ __global__ __launch_bounds__(256) void conv_gemm_x3_kernel(GArgs a) {
   }
 }
 
-template <int KH, int KW, int BM, int MODE, bool FAST>
+template <int KH, int KW, int BM, int MODE, bool FAST, bool TAPK = false>
 void launch_f(hipStream_t s, const GArgs& a, dim3 grid) {
   constexpr int AH = 2 * (BM / 32) * 2 * 512, BH = 2 * 2 * BN * 16;
   const size_t lds = (size_t)2 * (AH + BH) * sizeof(_Float16);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_x3_kernel<KH, KW, BM, MODE, FAST>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_gemm_x3_kernel<KH, KW, BM, MODE, FAST, TAPK>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((conv_gemm_x3_kernel<KH, KW, BM, MODE, FAST>), grid, dim3(256), lds, s, a);
+  hipLaunchKernelGGL((conv_gemm_x3_kernel<KH, KW, BM, MODE, FAST, TAPK>), grid, dim3(256), lds, s, a);
+}
+
+// the tap-major gather (TAPK above): a tap-major packing, whole 8-channel groups per source,
+// every pixel's byte offset (frame base included) below 2^32
+bool gemm_tapk_ok(const GArgs& a, int two) {
+  static const bool off = [] { const char* v = getenv("EXTDM_GEMM_NOTAPK"); return v && v[0] && v[0] != '0'; }();
+  if (off || !a.wt || a.Cin % 8 != 0 || a.C0 % 8 != 0) return false;
+  auto ext = [&](long sb, long sc, long st, int C) {
+    return ((long)(a.B - 1) * sb + (long)(C - 1) * sc + (long)(a.T - 1) * st + (long)a.Hin * a.Win) * 4;
+  };
+  // the pixel part of an offset: (b, t) frame base + in-plane position (channel 0); the
+  // soffset of channel 7 of a group
+  const long e0 = ext(a.i0b, 0, a.i0t, 1), e1 = two ? ext(a.i1b, 0, a.i1t, 1) : 0;
+  const long c7 = 7 * 4 * std::max(a.i0c, two ? a.i1c : 0L);
+  return e0 + c7 < (1L << 32) - 1 && e1 + c7 < (1L << 32) - 1 && c7 < (1L << 31);
 }
 
 // the fast gather (FAST above): taps that repeat per K tile, one source, 31-bit byte offsets
@@ -315,7 +366,16 @@ int gemm_in_bytes(const GArgs& a) {
 }
 
 template <int KH, int KW, int BM, int MODE>
-void launch(hipStream_t s, const GArgs& a, dim3 grid) {
+void launch(hipStream_t s, const GArgs& a, dim3 grid, bool two) {
+  if constexpr (BK % (KH * KW) != 0 || MODE == MODE_UP2) {
+    if (gemm_tapk_ok(a, two)) {
+      GArgs f = a;
+      f.w = a.wt;
+      f.nkt = a.nkt_t;
+      launch_f<KH, KW, BM, MODE, false, true>(s, f, grid);
+      return;
+    }
+  }
   if constexpr (BK % (KH * KW) == 0 && MODE != MODE_UP2) {
     if (gemm_fast_ok(a, KH * KW, MODE)) {
       GArgs f = a;
@@ -328,10 +388,10 @@ void launch(hipStream_t s, const GArgs& a, dim3 grid) {
 }
 
 template <int KH, int KW, int MODE>
-bool launch_bm(hipStream_t s, const GArgs& a, int bm, dim3 grid) {
-  if (bm == 128) launch<KH, KW, 128, MODE>(s, a, grid);
-  else if (bm == 64) launch<KH, KW, 64, MODE>(s, a, grid);
-  else if (bm == 32) launch<KH, KW, 32, MODE>(s, a, grid);
+bool launch_bm(hipStream_t s, const GArgs& a, int bm, dim3 grid, bool two) {
+  if (bm == 128) launch<KH, KW, 128, MODE>(s, a, grid, two);
+  else if (bm == 64) launch<KH, KW, 64, MODE>(s, a, grid, two);
+  else if (bm == 32) launch<KH, KW, 32, MODE>(s, a, grid, two);
   else return false;
   return true;
 }
@@ -356,6 +416,8 @@ bool conv_gemm_x3_forward(hipStream_t s, const View& out, const View& in0, const
   a.e = epi;
   a.OWfull = out.W;
   a.range = x3_range_ptr();
+  a.wt = reinterpret_cast<const _Float16*>(w.gxt);
+  a.nkt_t = w.gnkt_t;
   if (w.mode == MODE_DECONV) { a.Ho = in0.H; a.Wo = in0.W; }
   else { a.Ho = out.H; a.Wo = out.W; }
   a.N = (long)a.B * a.T * a.Ho * a.Wo;
@@ -364,17 +426,17 @@ bool conv_gemm_x3_forward(hipStream_t s, const View& out, const View& in0, const
   dim3 grid((unsigned)((a.N + BN - 1) / BN), (unsigned)((w.M + bm - 1) / bm), w.mode == MODE_DECONV ? 4 : 1);
   const int kh = w.KH, kw = w.KW, mode = w.mode;
   if (mode == MODE_DECONV) {
-    if (kh == 2 && kw == 2) return launch_bm<2, 2, MODE_DECONV>(s, a, bm, grid);
+    if (kh == 2 && kw == 2) return launch_bm<2, 2, MODE_DECONV>(s, a, bm, grid, in1 != nullptr);
     return false;
   }
   if (mode == MODE_UP2) {
-    if (kh == 3 && kw == 3) return launch_bm<3, 3, MODE_UP2>(s, a, bm, grid);
+    if (kh == 3 && kw == 3) return launch_bm<3, 3, MODE_UP2>(s, a, bm, grid, in1 != nullptr);
     return false;
   }
-  if (kh == 1 && kw == 1) return launch_bm<1, 1, MODE_CONV>(s, a, bm, grid);
-  if (kh == 3 && kw == 3) return launch_bm<3, 3, MODE_CONV>(s, a, bm, grid);
-  if (kh == 4 && kw == 4) return launch_bm<4, 4, MODE_CONV>(s, a, bm, grid);
-  if (kh == 7 && kw == 7) return launch_bm<7, 7, MODE_CONV>(s, a, bm, grid);
+  if (kh == 1 && kw == 1) return launch_bm<1, 1, MODE_CONV>(s, a, bm, grid, in1 != nullptr);
+  if (kh == 3 && kw == 3) return launch_bm<3, 3, MODE_CONV>(s, a, bm, grid, in1 != nullptr);
+  if (kh == 4 && kw == 4) return launch_bm<4, 4, MODE_CONV>(s, a, bm, grid, in1 != nullptr);
+  if (kh == 7 && kw == 7) return launch_bm<7, 7, MODE_CONV>(s, a, bm, grid, in1 != nullptr);
   return false;
 }
 

@@ -151,6 +151,10 @@ struct PackedW {
   void* gx = nullptr;
   float* gscale = nullptr;
   int gbm = 0, gnkt = 0;
+  // the same with K tap-major (k = (ky * KW + kx) * Cin + ci; Cin % 8 == 0, KH * KW not dividing
+  // 32): the gather of a K tile's 8-channel groups shares one tap (conv_gemm_x3.hip TAPK)
+  void* gxt = nullptr;
+  int gnkt_t = 0;
   // fp32 direct VALU layout [group][ci][ky * KW + kx][vcot rounded up to 4] (conv_narrow.hip), zero past M:
   // KS x KS convs with few output channels
   float* wv = nullptr;

@@ -218,27 +218,38 @@ struct ExtdmHandle {
       scale[m] = std::ldexp(1.f, e);
       rs[m] = std::ldexp(1.f, -e);
     }
-    std::vector<_Float16> g((size_t)npar * mt * nkt * ah, (_Float16)0.f);
-    for (int par = 0; par < npar; ++par)
-      for (int mtile = 0; mtile < mt; ++mtile)
-        for (int kt = 0; kt < nkt; ++kt)
-          for (int st = 0; st < 2; ++st)
-            for (int q = 0; q < m32; ++q)
-              for (int l = 0; l < 64; ++l)
-                for (int e = 0; e < 8; ++e) {
-                  const int m = mtile * bm + q * 32 + (l & 31), k = kt * 32 + st * 16 + 8 * (l >> 5) + e;
-                  if (m >= M || k >= K) continue;
-                  const float v = a[par * plane + (size_t)k * pw.Mpad + m] * scale[m];
-                  const _Float16 hi = (_Float16)v;
-                  const size_t base = (((size_t)par * mt + mtile) * nkt + kt) * ah + (size_t)((st * m32 + q) * 2) * 512;
-                  g[base + l * 8 + e] = hi;
-                  g[base + 512 + l * 8 + e] = (_Float16)(v - (float)hi);
-                }
-    pw.gx = dmalloc(g.size() * sizeof(_Float16));
-    HIPCHK(hipMemcpy(pw.gx, g.data(), g.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+    // kmap(k): the row of `a` GEMM row k of this packing reads (identity: ci-major; the
+    // tap-major copy below: k = tap * ci + c -> c * KK + tap)
+    auto pack = [&](auto kmap) {
+      std::vector<_Float16> g((size_t)npar * mt * nkt * ah, (_Float16)0.f);
+      for (int par = 0; par < npar; ++par)
+        for (int mtile = 0; mtile < mt; ++mtile)
+          for (int kt = 0; kt < nkt; ++kt)
+            for (int st = 0; st < 2; ++st)
+              for (int q = 0; q < m32; ++q)
+                for (int l = 0; l < 64; ++l)
+                  for (int e = 0; e < 8; ++e) {
+                    const int m = mtile * bm + q * 32 + (l & 31), k = kt * 32 + st * 16 + 8 * (l >> 5) + e;
+                    if (m >= M || k >= K) continue;
+                    const float v = a[par * plane + (size_t)kmap(k) * pw.Mpad + m] * scale[m];
+                    const _Float16 hi = (_Float16)v;
+                    const size_t base = (((size_t)par * mt + mtile) * nkt + kt) * ah + (size_t)((st * m32 + q) * 2) * 512;
+                    g[base + l * 8 + e] = hi;
+                    g[base + 512 + l * 8 + e] = (_Float16)(v - (float)hi);
+                  }
+      void* d = dmalloc(g.size() * sizeof(_Float16));
+      HIPCHK(hipMemcpy(d, g.data(), g.size() * sizeof(_Float16), hipMemcpyHostToDevice));
+      return d;
+    };
+    pw.gx = pack([](int k) { return k; });
     pw.gscale = dmalloc(M * sizeof(float));
     HIPCHK(hipMemcpy(pw.gscale, rs.data(), M * sizeof(float), hipMemcpyHostToDevice));
     pw.gbm = bm; pw.gnkt = nkt;
+    const int kk = pw.KH * pw.KW, ci = K / kk;
+    if (npar == 1 && kk > 1 && 32 % kk != 0 && ci % 8 == 0) {
+      pw.gxt = pack([&](int k) { const int tap = k / ci, c = k - tap * ci; return c * kk + tap; });
+      pw.gnkt_t = nkt;
+    }
   }
   // f16x3 layout (conv_x3.hip): [mtile][cb*KS + ky][(g, kx)][m32][hi|lo][lane][8], lane =
   // (h, lc): row m = mtile*BM + m32*32 + lc, input channel cb*16NG + g*16 + 8h + e. Row m is
