@@ -127,7 +127,7 @@ WORKLOADS = {
     'kth': dict(image=64, tc=10, tp=20, total_pred=40, sampling_steps=100, timesteps=1000, batch=16, occ=False,
                 precision=None, cpu_steady=2, baseline='configs[2]: KTH 64x64 ch1, cond=10 pred=40, DDIM 100 steps, batch=64 on 4 GPUs',
                 lead=(6, 'level-0 shifted STW attention (ada 4x4x4 windows, dim_head 16), fused LN/qkv/RoPE/softmax/PV/proj')),
-    'cityscapes': dict(image=128, tc=2, tp=5, total_pred=28, sampling_steps=1000, timesteps=1000, batch=64, occ=True,
+    'cityscapes': dict(image=128, tc=2, tp=5, total_pred=28, sampling_steps=1000, timesteps=1000, batch=128, occ=True,
                        precision=None, cpu_steady=2, baseline='configs[3]: Cityscapes 128x128 ch3, cond=2 pred=28, DDPM 1000 steps',
                        lead=(6, 'level-0 shifted STW attention (ada_u22 4x4x4 windows, dim_head 32), fused LN/qkv/RoPE/softmax/PV/proj')),
     'ucf': dict(image=256, tc=4, tp=12, total_pred=12, sampling_steps=10, timesteps=1000, batch=8, occ=True,
