@@ -1460,7 +1460,7 @@ struct ExtdmHandle {
       // cat(cond_frames[:, :, :-1], x) ++ cond_fea at latent resolution (wo_ref.py:911-921)
       REQUIRE(fs == L, "wo_ref: cond_fea must be at the latent resolution");
       const View fc = vf.frames(0, tc);
-      conv(r, vc.frames(0, tc), &fc, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+      init_conv_cond(r, vc.frames(0, tc), fc);
       hoist_fea(B, vf.frames(tc, cfg.tp));
       return;
     }
@@ -1481,12 +1481,32 @@ struct ExtdmHandle {
     hoist_fea(B, arch == EXTDM_ARCH_ADA && fa_all.p ? with_batch(fa_all, B).frames(tc, cfg.tp)
                                                      : with_batch(fup_all, B).frames(tc, cfg.tp));
     if (arch == EXTDM_ARCH_ADA_U22) {  // no init_noise_conv (ada_u22.py:1180)
-      conv(r, vc, &fup, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
+      init_conv_cond(r, vc, fup);
     } else {
       View x0 = alloc_cf(B, 256, tc, L, L);
       conv(x0, vc, nullptr, P("init_noise_conv.weight"), 1, 3, D("init_noise_conv.bias"));
       conv(r, x0, &fup, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
     }
+  }
+
+  // init_conv over cat(x, f) for the cond frames (wo_ref / ada_u22). With the hoisted split (the
+  // step's form): the cond_fea branch + bias (a channel count the tap-major GEMM gathers), then
+  // the 3-channel x-branch added on f16x3 MFMA -- the two-source conv's 3 + C channels were
+  // left to the per-element gather (UCF: 9.1 ms per sampling call at 8 clips)
+  void init_conv_cond(const View& r, const View& x, const View& f) {
+    if (fea_hoist_on() && conv7c3_on(r)) {
+      split_init_conv(3);
+      conv(r, f, nullptr, P("init_conv.weight#f"), 1, 3, D("init_conv.bias"));
+      const XPathW& cw = Pconv7c3();
+      Scope sc(arena);
+      View xpad = alloc_cf(x.B, 3, x.T, xpad_size(x.H), xpad_size(x.W));
+      if (!plan) {
+        xpad_forward(s, xpad, x);
+        REQUIRE(conv7c3_x3_forward(s, r, xpad, cw.w, cw.rs, nullptr, &r), "init_conv x-branch launch rejected");
+      }
+      return;
+    }
+    conv(r, x, &f, P("init_conv.weight"), 1, 3, D("init_conv.bias"));
   }
 
   // fr_all = init_conv's cond_fea branch over the tp predicted frames (fea_hoist_on): f is the
