@@ -199,12 +199,13 @@ bool narrow_off() {
 
 int narrow_cot(int KS, int M) {
   if (KS != 7 || !(M <= 16 || (M % 32 != 0 && M <= 80))) return 0;
+  // fewest padded rows, each group's input staging priced at two output channels' FMAs
   static const int cands[] = {16, 13, 8, 4, 3, 2, 1};
   int best = 0;
-  long bestpad = 1L << 30;
+  long bestcost = 1L << 30;
   for (int c : cands) {
-    const long pad = (long)(M + c - 1) / c * c;
-    if (pad < bestpad) { bestpad = pad; best = c; }
+    const long groups = (M + c - 1) / c, cost = groups * c + 2 * groups;
+    if (cost < bestcost) { bestcost = cost; best = c; }
   }
   return best;
 }
