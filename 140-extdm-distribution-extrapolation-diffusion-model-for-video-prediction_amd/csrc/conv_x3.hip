@@ -937,10 +937,35 @@ void launch_ns(hipStream_t s, const X3Args& a, unsigned ntiles) {
 // workgroup count at the reference batch 64), never of the batch: a clip's result must
 // not depend on the shard it lands in (every output element sums the same slices in the same
 // order whichever tile, and whichever tile-mates, it has). EXTDM_NO_SPLITK=1 turns it off (A/B).
+// Long-K 256-row 1x1 convs (>= 128 channel blocks, K >= 4096: KTH's 7680 -> 5120 Tmodulators,
+// 40 workgroups at its 16 clips per GPU): the slice count minimises a cost model at a reference
+// batch of 16 clips (KTH's 64 on 4 GPUs) — ceil(S x workgroups / 256) rounds of ncgb / S channel
+// blocks (1.74 us each on the 256 x 128 tile) plus S partial planes written and summed back (1.5 TB/s
+// effective), both measured on KTH's level-2 Tmodulator (417 us unsplit, 364 us at S = 3) — a
+// function of the per-sample geometry only, like the rule above. x3_bn256 keeps these convs
+// on the 256 x 128 tile, so the split never depends on the launch's batch.
+// EXTDM_X3_LONGK=0 turns it off (A/B).
+constexpr int kLongKBlocks = 128;
+int split_slices_longk(const X3Args& a) {
+  static const bool on = [] { const char* v = getenv("EXTDM_X3_LONGK"); return !(v && v[0] == '0'); }();
+  if (!on || a.ncgb < kLongKBlocks || a.P < 1) return 0;
+  const long nwg16 = (16L * a.T + a.NP - 1) / a.NP * a.nrow_tiles * ((a.Cout + 255) / 256);
+  const double blk_us = 1.74;
+  const double part_us = (double)a.Cout * (16.0 * a.T * a.H * a.W) * 8.0 / 1.5e6;
+  int best = 1;
+  double bc = 1e300;
+  for (int S = 1; S <= a.ncgb / 16; ++S) {
+    const double c = (double)((nwg16 * S + 255) / 256) * ((a.ncgb + S - 1) / S) * blk_us + (S > 1 ? S * part_us : 0.0);
+    if (c < bc * 0.999) { bc = c; best = S; }
+  }
+  return best >= 2 ? best : 0;
+}
+
 int split_slices(const X3Args& a, unsigned ntiles, long max_wg, long max_total, int bm = 128) {
   static const bool off = [] { const char* v = getenv("EXTDM_NO_SPLITK"); return v && v[0] && v[0] != '0'; }();
   (void)ntiles;
   if (off || a.ncgb < 4 || a.P < 1) return 0;
+  if (bm == 256 && a.ncgb >= kLongKBlocks) return split_slices_longk(a);
   // workgroups of this conv at the reference batch 64 (a function of the per-sample geometry:
   // T frames per sample, NP planes and nrow_tiles row tiles per tile; single-frame views such as
   // the Tmodulator's '(T C)' GEMM put several samples in one tile, which is still batch-independent)
@@ -1142,6 +1167,9 @@ bool x3_mfast(const X3Args& a, const X3Tile& tl, unsigned ntiles) {
 bool x3_bn256(const View& out, const PackedW& w, const ConvEpi& epi) {
   static const int bn1 = [] { const char* v = getenv("EXTDM_X3_BN1"); return v ? atoi(v) : 256; }();
   if ((bn1 != 256 && bn1 != 64) || w.KH != 1 || w.xbm != 256 || w.xbn != 128 || epi.res_aff) return false;
+  // long-K convs stay on the 256 x 128 tile and its batch-independent split-K (split_slices_longk)
+  static const bool longk = [] { const char* v = getenv("EXTDM_X3_LONGK"); return !(v && v[0] == '0'); }();
+  if (longk && w.xncgb >= kLongKBlocks) return false;
   const int H = out.H, W = out.W;
   if (W > 256 || 256 % W != 0) return false;
   const int TH = std::min(H, 256 / W);

@@ -43,6 +43,27 @@ def _handle(cfg, timesteps, B, precision=None):
     return h
 
 
+def test_kth_unet_batch_slice_bitwise():
+    """The KTH denoiser (ada, 10 -> 20) at its bench batch of 16 clips, at 64 and one clip alone: eps
+    bitwise equal per clip. Its 7680 -> 5120 Tmodulators run split-K with a slice count fixed by the
+    per-sample geometry (conv_x3.hip split_slices_longk) and never on the batch-chosen 256 x 256 tile,
+    so shards of a batch sum every output in the same order as the unsharded run."""
+    cfg = E2E['kth_ddim100']['unet']
+    x, _, cond, fea = unet_inputs(cfg, B=64, seed=23)
+    tt = torch.full((64,), 433, dtype=torch.long)
+    eps = {}
+    for B in (64, 16, 1):
+        h = _handle(cfg, 1000, B)
+        e = torch.empty((B,) + tuple(x.shape[1:]), device=DEV)
+        h.unet_forward(x[:B].contiguous().to(DEV), tt[:B].contiguous().to(DEV), cond[:B].contiguous().to(DEV),
+                       fea[:B].contiguous().to(DEV), e)
+        torch.cuda.synchronize()
+        eps[B] = e.cpu()
+        del h
+    assert torch.equal(eps[64][:16], eps[16])
+    assert torch.equal(eps[16][:1], eps[1])
+
+
 def test_kth_ddim100_chain_vs_reference():
     c = E2E['kth_ddim100']
     cfg = c['unet']
